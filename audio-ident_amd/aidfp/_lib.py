@@ -1,0 +1,113 @@
+"""ctypes binding of libaidfp.so (include/aidfp.h).
+
+The library is the product path: if it is missing or fails to load, every
+engine call raises ``EngineUnavailable`` -- there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(os.environ.get("AIDFP_LIB", Path(__file__).resolve().parent / "libaidfp.so"))
+
+AID_OK = 0
+AID_ERR_INVALID = -1
+AID_ERR_DEVICE = -2
+AID_ERR_NOMEM = -3
+AID_ERR_STATE = -4
+AID_PCM_HOST = 0
+AID_PCM_DEVICE = 1
+AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH = range(5)
+AID_K_COUNT = 5
+KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth"]
+
+
+class EngineUnavailable(RuntimeError):
+    """libaidfp.so could not be loaded or the GPU could not be initialised."""
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"aidfp error {code}: {msg}")
+        self.code = code
+
+
+class AidConfig(ctypes.Structure):
+    _fields_ = [
+        ("sample_rate", ctypes.c_int32),
+        ("hop", ctypes.c_int32),
+        ("peak_threshold", ctypes.c_float),
+        ("device", ctypes.c_int32),
+        ("min_match", ctypes.c_int32),
+        ("max_results", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 10),
+    ]
+
+
+class AidHash(ctypes.Structure):
+    _fields_ = [("hash", ctypes.c_uint32), ("t1", ctypes.c_uint32)]
+
+
+# (name, restype, argtypes) for every symbol include/aidfp.h declares
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+SIGNATURES = [
+    ("aid_abi_version", I32, []),
+    ("aid_last_error", ctypes.c_char_p, []),
+    ("aid_config_default", ctypes.c_int, [I32, P]),
+    ("aid_engine_create", ctypes.c_int, [P, P]),
+    ("aid_engine_destroy", None, [P]),
+    ("aid_engine_config", ctypes.c_int, [P, P]),
+    ("aid_num_frames", I64, [P, I64]),
+    ("aid_hash_capacity", I64, [P, I64]),
+    ("aid_extract", ctypes.c_int, [P, P, P, I32, I32, P]),
+    ("aid_sync", ctypes.c_int, [P]),
+    ("aid_result_counts", ctypes.c_int, [P, P]),
+    ("aid_result_hashes", ctypes.c_int, [P, I32, P, I64, P]),
+    ("aid_result_device", ctypes.c_int, [P, P, P, P, P]),
+    ("aid_result_power", ctypes.c_int, [P, I32, P, I64]),
+    ("aid_result_peakmask", ctypes.c_int, [P, I32, P, I64]),
+    ("aid_spectrogram", ctypes.c_int, [P, P, I64, P, I64]),
+    ("aid_synth", ctypes.c_int, [P, P, P, P, I32, I64, I32, ctypes.c_uint32, P]),
+    ("aid_profile_enable", ctypes.c_int, [P, I32]),
+    ("aid_profile_read", ctypes.c_int, [P, P, P, I32]),
+]
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise EngineUnavailable(f"{LIB_PATH} not built (run __graft_entry__.build())")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7. Loading torch
+        # first makes the dynamic loader bind libaidfp's NEEDED libamdhip64.so.7 to that same
+        # copy (SONAME match); loading ours first would put two runtimes in the process.
+        try:
+            import torch  # noqa: F401  (plumbing: device memory, streams, RCCL)
+        except ImportError:  # pragma: no cover - torch is part of the image
+            pass
+        try:
+            L = ctypes.CDLL(str(LIB_PATH))
+        except OSError as exc:  # pragma: no cover - depends on the box
+            raise EngineUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    msg = load().aid_last_error()
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int) -> None:
+    if rc != AID_OK:
+        raise EngineError(rc, last_error())

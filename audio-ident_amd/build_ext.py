@@ -1,0 +1,69 @@
+"""Build libaidfp.so (HIP, gfx950) in-tree: audio-ident_amd/aidfp/libaidfp.so.
+
+One hipcc invocation per translation unit (parallel), then one link. Flags:
+``-ffp-contract=off`` is load-bearing: spec/FPSPEC.md pins every binary32 op,
+so hipcc must not fuse a multiply and an add on its own.
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "build"
+LIB = PKG / "aidfp" / "libaidfp.so"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "engine.cpp"]
+FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    "-Wall",
+    "-Wno-unused-result",
+]
+
+
+def _deps(src: Path) -> list[Path]:
+    return [src] + sorted(CSRC.glob("*.h")) + [PKG.parent / "include" / "aidfp.h"]
+
+
+def _compile(name: str, verbose: bool) -> Path:
+    src = CSRC / name
+    obj = OBJ / (name + ".o")
+    if obj.exists() and all(d.stat().st_mtime <= obj.stat().st_mtime for d in _deps(src)):
+        return obj
+    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+    if name.endswith(".cpp"):
+        cmd = [HIPCC, *FLAGS, "-x", "hip", "-c", str(src), "-o", str(obj)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def build(verbose: bool = False) -> Path:
+    OBJ.mkdir(exist_ok=True)
+    srcs = [s for s in SOURCES if (CSRC / s).exists()]
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
+    if LIB.exists() and all(o.stat().st_mtime <= LIB.stat().st_mtime for o in objs):
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

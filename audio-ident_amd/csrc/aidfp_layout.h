@@ -1,0 +1,45 @@
+// aidfp_layout.h -- HBM layout constants shared by host (engine.cpp) and kernels.
+#pragma once
+#include <stdint.h>
+
+namespace aid {
+
+constexpr int kN = 2048;          // FFT length (FPSPEC 1)
+constexpr int kBins = 1024;       // bins kept per frame
+constexpr int kPeakDT = 7;        // peak neighbourhood, frames
+constexpr int kPeakDF = 15;       // peak neighbourhood, bins
+constexpr int kZoneDT = 63;       // target zone, frames
+constexpr int kZoneDF = 127;      // target zone, bins
+constexpr int kFan = 10;          // targets per anchor
+constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
+
+// K1: frames per workgroup (4 waves x kStftFramesPerWave)
+constexpr int kStftWaves = 4;
+constexpr int kStftFramesPerWave = 16;
+constexpr int kStftFramesPerBlock = kStftWaves * kStftFramesPerWave;
+constexpr int kStftLdsPerWave = 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024+32)
+
+// K2: output frames per workgroup strip
+constexpr int kPeakStrip = 128;
+
+// K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
+constexpr int kHashChunk = 1024;
+constexpr int kHashChunkPeakCap = 64 * ((kHashChunk + kZoneDT + 7) / 8);
+
+inline int64_t num_frames(int64_t n, int hop) { return (hop <= 0 || n < kN) ? 0 : 1 + (n - kN) / hop; }
+inline int64_t peak_capacity(int64_t F) { return 64 * ((F + 7) / 8); }
+inline int64_t hash_capacity(int64_t F) { return kFan * peak_capacity(F); }
+
+// Per-clip descriptor uploaded with each extraction call (struct of 8 x int64).
+struct ClipDesc {
+    int64_t pcm_off;     // first sample of the clip in the PCM buffer (even)
+    int64_t frames;      // F
+    int64_t frame_base;  // first row of the clip in the power plane / mask plane
+    int64_t strip_base;  // first K2 strip of the clip
+    int64_t chunk_base;  // first K3 chunk of the clip
+    int64_t hash_base;   // first record slot of the clip in the output buffer
+    int64_t hash_cap;    // record capacity of the clip
+    int64_t reserved;
+};
+
+}  // namespace aid

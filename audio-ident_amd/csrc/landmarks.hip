@@ -1,0 +1,170 @@
+// landmarks.hip -- K3 `landmark_hash`: peak compaction + anchor->target pairing +
+// 32-bit hash pack (FPSPEC 5 ordering, FPSPEC 6 hashing).
+//
+// Replaces the hash stage inside the external `olaf_c` binary (SURVEY.md 8a row
+// a3; reference call sites fingerprint.py:117-125, 185-193).
+//
+// Unit = (clip, chunk of kHashChunk anchor frames). A workgroup:
+//   1. popcounts the 16 mask words of every frame in [c0, min(c1+63, F)) and
+//      block-scans the counts (frame -> first peak index);
+//   2. expands the masks into an LDS peak list packed (frame << 10 | bin), which
+//      is already in (t, k) order -- exactly the target order of FPSPEC 6;
+//   3. gives each thread a contiguous run of anchors; a thread walks forward from
+//      each anchor while t2 - t1 <= 63 and keeps the first 10 targets with
+//      |k2 - k1| <= 127.
+// Pass COUNT writes the chunk's record total; pass WRITE re-derives its base from
+// the totals of the clip's earlier chunks, block-scans per-thread totals and
+// stores records {hash, t1} in canonical order. Chunk 0 of a clip also writes
+// the clip's record count.
+#include "aidfp_device.h"
+
+namespace aid {
+
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[256+1]*/, int64_t *total) {
+    const int tid = threadIdx.x;
+    tmp[tid] = v;
+    __syncthreads();
+    // Hillis-Steele over 256 entries (small; runs once per phase)
+    for (int off = 1; off < 256; off <<= 1) {
+        const int64_t add = tid >= off ? tmp[tid - off] : 0;
+        __syncthreads();
+        tmp[tid] += add;
+        __syncthreads();
+    }
+    const int64_t incl = tmp[tid];
+    if (total) *total = tmp[255];
+    __syncthreads();
+    return incl - v;
+}
+
+__device__ __forceinline__ uint32_t make_hash(int k1, int k2, int dt) {
+    return ((uint32_t)(k1 & 0x3FF) << 22) | ((uint32_t)(k2 & 0x3FF) << 12) | ((uint32_t)dt & 0xFFF);
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ mask, const ClipDesc *__restrict__ clips,
+                                                  int n_clips, int64_t total_chunks, int64_t *__restrict__ chunk_counts,
+                                                  uint64_t *__restrict__ records, int64_t *__restrict__ clip_counts) {
+    __shared__ uint32_t plist[kHashChunkPeakCap];
+    __shared__ uint32_t foff[kHashChunk + kZoneDT + 2];
+    __shared__ int64_t scan_tmp[256];
+    const int tid = threadIdx.x;
+    const int64_t chunk = blockIdx.x;
+    if (chunk >= total_chunks) return;
+    int lo = 0, hi = n_clips - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (clips[mid].chunk_base <= chunk) lo = mid; else hi = mid - 1;
+    }
+    const ClipDesc cd = clips[lo];
+    const int64_t F = cd.frames;
+    const int64_t q = chunk - cd.chunk_base;
+    const int64_t c0 = q * kHashChunk;
+    const int64_t c1 = min(c0 + (int64_t)kHashChunk, F);
+    const int64_t g1 = min(c1 + (int64_t)kZoneDT, F);
+    const int nf = (int)(g1 - c0);
+    const uint64_t *Mc = mask + (cd.frame_base + c0) * kMaskWords;
+
+    // 1. per-frame counts over a contiguous run of frames per thread, block scan
+    const int per = (nf + 255) / 256;
+    const int fa = min(tid * per, nf), fz = min(fa + per, nf);
+    int64_t mine = 0;
+    for (int f = fa; f < fz; ++f) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kMaskWords; ++w) c += __popcll(Mc[f * kMaskWords + w]);
+        foff[f] = c;
+        mine += c;
+    }
+    int64_t npk = 0;
+    int64_t run = block_excl_scan(mine, scan_tmp, &npk);
+    // 2. expand to the (t,k)-ordered peak list
+    for (int f = fa; f < fz; ++f) {
+        const uint32_t c = foff[f];
+        int64_t idx = run;
+        for (int w = 0; w < kMaskWords; ++w) {
+            uint64_t m = Mc[f * kMaskWords + w];
+            while (m) {
+                const int bpos = __ffsll((unsigned long long)m) - 1;
+                plist[idx++] = ((uint32_t)f << 10) | (uint32_t)(64 * w + bpos);
+                m &= m - 1;
+            }
+        }
+        foff[f] = (uint32_t)run;
+        run += c;
+    }
+    if (tid == 0) foff[nf] = (uint32_t)npk;
+    __syncthreads();
+    const int n_anchor = (int)foff[c1 - c0];
+
+    // 3. anchors: contiguous run per thread
+    const int pa_per = (n_anchor + 255) / 256;
+    const int aa = min(tid * pa_per, n_anchor), az = min(aa + pa_per, n_anchor);
+    int64_t my = 0;
+    for (int i = aa; i < az; ++i) {
+        const uint32_t a = plist[i];
+        const int ta = (int)(a >> 10), ka = (int)(a & 1023);
+        int got = 0;
+        for (int j = i + 1; j < (int)npk && got < kFan; ++j) {
+            const uint32_t b = plist[j];
+            const int dt = (int)(b >> 10) - ta;
+            if (dt > kZoneDT) break;
+            if (dt <= 0) continue;
+            const int df = (int)(b & 1023) - ka;
+            if (df < -kZoneDF || df > kZoneDF) continue;
+            ++got;
+        }
+        my += got;
+    }
+    int64_t chunk_total = 0;
+    const int64_t excl = block_excl_scan(my, scan_tmp, &chunk_total);
+    if constexpr (!WRITE) {
+        if (tid == 0) chunk_counts[chunk] = chunk_total;
+    } else {
+        // base of this chunk inside the clip = sum of the clip's earlier chunks
+        int64_t pre = 0;
+        for (int64_t c = cd.chunk_base + tid; c < chunk; c += 256) pre += chunk_counts[c];
+        int64_t before = 0;
+        block_excl_scan(pre, scan_tmp, &before);
+        if (q == 0) {
+            int64_t all = 0;
+            const int64_t nck = (F + kHashChunk - 1) / kHashChunk;
+            for (int64_t c = cd.chunk_base + tid; c < cd.chunk_base + nck; c += 256) all += chunk_counts[c];
+            int64_t tot = 0;
+            block_excl_scan(all, scan_tmp, &tot);
+            if (tid == 0) clip_counts[lo] = tot;
+        }
+        uint64_t *out = records + cd.hash_base + before + excl;
+        int64_t o = 0;
+        for (int i = aa; i < az; ++i) {
+            const uint32_t a = plist[i];
+            const int ta = (int)(a >> 10), ka = (int)(a & 1023);
+            const uint64_t t1 = (uint64_t)(c0 + ta) << 32;
+            int got = 0;
+            for (int j = i + 1; j < (int)npk && got < kFan; ++j) {
+                const uint32_t b = plist[j];
+                const int dt = (int)(b >> 10) - ta;
+                if (dt > kZoneDT) break;
+                if (dt <= 0) continue;
+                const int kb = (int)(b & 1023);
+                const int df = kb - ka;
+                if (df < -kZoneDF || df > kZoneDF) continue;
+                out[o++] = t1 | make_hash(ka, kb, dt);
+                ++got;
+            }
+        }
+    }
+}
+
+void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
+                      int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s) {
+    if (total_chunks <= 0) return;
+    if (write)
+        hipLaunchKernelGGL(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(256), 0, s, mask, clips, n_clips,
+                           total_chunks, chunk_counts, records, clip_counts);
+    else
+        hipLaunchKernelGGL(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(256), 0, s, mask, clips, n_clips,
+                           total_chunks, chunk_counts, records, clip_counts);
+}
+
+}  // namespace aid

@@ -1,0 +1,126 @@
+/*
+ * aidfp.h -- C ABI of the MI355X fingerprint engine (libaidfp.so, gfx950).
+ *
+ * This is the drop-in boundary that replaces the process boundary of the
+ * reference: audio-ident-service/app/audio/fingerprint.py spawns `olaf_c`
+ * (store :117-125, query :185-193, del :239-246) with env OLAF_DB (:71-84) and
+ * parses its stdout CSV (:273-350). Here the same three operations are plain C
+ * calls on caller-owned buffers; the Python adapter
+ * (audio-ident_amd/aidfp/fingerprint.py) keeps the reference's async API on top.
+ *
+ * Conventions: every function returns AID_OK (0) or a negative AID_ERR_*;
+ * aid_last_error() returns a thread-local message for the last failure. Pointers
+ * are plain host or device pointers as documented per call; `stream` is a
+ * hipStream_t passed as void* (NULL = the engine's own stream). An engine is
+ * bound to one GPU; calls on one engine must be serialised by the caller except
+ * where noted (the Python adapter holds a lock, like the reference's single
+ * LMDB writer, fingerprint.py:7-8).
+ */
+#ifndef AIDFP_H
+#define AIDFP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AID_ABI_VERSION 1
+
+#define AID_OK 0
+#define AID_ERR_INVALID (-1)  /* bad argument */
+#define AID_ERR_DEVICE (-2)   /* HIP runtime / device failure: engine unusable */
+#define AID_ERR_NOMEM (-3)    /* device or host allocation failed */
+#define AID_ERR_STATE (-4)    /* call out of order (e.g. no extraction yet) */
+
+#define AID_PCM_HOST 0
+#define AID_PCM_DEVICE 1
+
+/* kernel ids for aid_profile_read */
+#define AID_K_STFT 0
+#define AID_K_PEAKS 1
+#define AID_K_LANDMARK_COUNT 2
+#define AID_K_LANDMARK_WRITE 3
+#define AID_K_SYNTH 4
+#define AID_K_COUNT 5
+
+typedef struct aid_engine aid_engine;
+
+typedef struct aid_config {
+    int32_t sample_rate;   /* Hz; per-index property */
+    int32_t hop;           /* 0 = FPSPEC default: 512 at sr >= 32 kHz, else 256 */
+    float peak_threshold;  /* 0 = FPSPEC default 4.0 */
+    int32_t device;        /* HIP device ordinal; -1 = current device */
+    int32_t min_match;     /* query: 0 = FPSPEC default 5 */
+    int32_t max_results;   /* query: 0 = FPSPEC default 50 */
+    int32_t reserved[10];
+} aid_config;
+
+/* one landmark record (FPSPEC 6): hash in the low word, anchor frame in the high word */
+typedef struct aid_hash {
+    uint32_t hash;
+    uint32_t t1;
+} aid_hash;
+
+int32_t aid_abi_version(void);
+const char *aid_last_error(void);
+
+/* Fill *out with the FPSPEC defaults for `sample_rate`. */
+int aid_config_default(int32_t sample_rate, aid_config *out);
+
+/* Create / destroy an engine (allocates device tables; workspaces grow on demand). */
+int aid_engine_create(const aid_config *cfg, aid_engine **out);
+void aid_engine_destroy(aid_engine *e);
+int aid_engine_config(const aid_engine *e, aid_config *out);
+
+/* Frames and worst-case record count of a clip of n samples (FPSPEC 1, 5). */
+int64_t aid_num_frames(const aid_engine *e, int64_t n_samples);
+int64_t aid_hash_capacity(const aid_engine *e, int64_t n_samples);
+
+/*
+ * Fingerprint extraction (K1 stft_power -> K2 peak_pick -> K3 landmark_hash).
+ * Clip c is pcm[offsets[c] .. offsets[c+1]); `offsets` is a HOST array of
+ * n_clips+1 non-decreasing sample indices. With AID_PCM_DEVICE, `pcm` is a device
+ * pointer and every offsets[c] must be even (8-byte aligned float2 frame loads);
+ * with AID_PCM_HOST the engine stages (and re-aligns) the samples itself.
+ * Asynchronous on `stream`; results stay on the device until fetched below.
+ * Replaces the FFT/peak/hash work of `olaf_c store|query` (fingerprint.py:117,185).
+ */
+int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t pcm_location,
+                void *stream);
+
+/* Block until the last extraction finished. */
+int aid_sync(aid_engine *e);
+
+/* Per-clip record counts of the last extraction (host array of n_clips). Synchronises. */
+int aid_result_counts(aid_engine *e, int64_t *counts);
+/* Copy clip `clip`'s records to host `out` (capacity `cap`); *n_out = count. Synchronises. */
+int aid_result_hashes(aid_engine *e, int32_t clip, aid_hash *out, int64_t cap, int64_t *n_out);
+/* Zero-copy device view of the last extraction: records (clip c starts at clip_base[c]),
+   per-clip counts (device int64[n_clips]); clip_base is a HOST array owned by the engine. */
+int aid_result_device(aid_engine *e, const aid_hash **records, const int64_t **counts_dev,
+                      const int64_t **clip_base_host, int32_t *n_clips);
+
+/* Debug/parity views of the last extraction (host copies, synchronise):
+   power rows [F][1024] fp32 of clip `clip`; peak bitmask [F][16] uint64. */
+int aid_result_power(aid_engine *e, int32_t clip, float *out, int64_t cap_floats);
+int aid_result_peakmask(aid_engine *e, int32_t clip, uint64_t *out, int64_t cap_words);
+
+/* Log-magnitude spectrogram 10*log10(P + 1e-10) of one host clip: out[F][1024] (host). */
+int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int64_t cap_floats);
+
+/* Deterministic synthetic PCM (aidfp/synth.py semantics) written to DEVICE `dst`
+   [n_clips][n]: tracks/starts are HOST arrays; noise_a = query-noise half-width (0 = none). */
+int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips, int64_t n,
+              int32_t noise_a, uint32_t salt, void *stream);
+
+/* Per-kernel timing with HIP events recorded on the launch stream. */
+int aid_profile_enable(aid_engine *e, int32_t on);
+/* ms[AID_K_COUNT] summed device time, launches[AID_K_COUNT]; synchronises; reset != 0 clears. */
+int aid_profile_read(aid_engine *e, double *ms, int64_t *launches, int32_t reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIDFP_H */

@@ -1,0 +1,95 @@
+"""GPU parity: K1-K3 through the C ABI vs the CPU oracle (bit-exact), and the
+GPU log-magnitude vs float64 numpy (tolerance, FPSPEC 4).
+
+The reference holds no golden vectors for this arithmetic (olaf_c is external,
+SURVEY.md 8c) -- parity is against oracle/fp_oracle.c, which tests/test_oracle.py
+pins to float64 numpy, a brute-force peak definition and known answers.
+"""
+
+import numpy as np
+import pytest
+
+import oracle as O
+from aidfp import synth
+from aidfp.engine import peaks_from_mask
+
+pytestmark = pytest.mark.gpu
+SR = 44100
+HOP = 512
+
+
+def _clip(tr, n, start=0, snr=None):
+    return synth.synth(tr, start, n, SR, snr_db=snr, salt=7)
+
+
+def test_power_bit_exact(gpu_engine):
+    clips = [_clip(1, 441000), _clip(2, 100000, start=12345, snr=20), _clip(3, 2048), _clip(4, 2049), _clip(5, 5000)]
+    gpu_engine.extract_host(clips)
+    for c, x in enumerate(clips):
+        P = gpu_engine.power(c, len(x))
+        R = O.stft_power(x, HOP)
+        assert P.shape == R.shape
+        assert np.array_equal(P.view(np.uint32), R.view(np.uint32)), f"clip {c}: power bits differ"
+
+
+def test_peaks_and_hashes_bit_exact(gpu_engine):
+    lens = [441000, 441000, 220500, 154350, 30000, 2047, 0, 2048 + 512 * 70]
+    clips = [_clip(10 + i, n, start=777 * i, snr=20 if i % 2 else None) for i, n in enumerate(lens)]
+    got = gpu_engine.extract_host(clips)
+    counts = gpu_engine.counts()
+    for c, x in enumerate(clips):
+        ref_pk = O.peaks(O.stft_power(x, HOP)) if len(x) >= 2048 else np.zeros((0, 2), np.int32)
+        pk = peaks_from_mask(gpu_engine.peakmask(c, len(x)))
+        assert np.array_equal(pk, ref_pk.reshape(-1, 2)), f"clip {c}: peaks differ"
+        ref = O.fingerprint(x, HOP)
+        assert counts[c] == len(ref)
+        assert np.array_equal(got[c], ref), f"clip {c}: hashes differ"
+
+
+def test_silence_and_tiny_inputs(gpu_engine):
+    clips = [np.zeros(44100, np.float32), np.zeros(0, np.float32), np.ones(100, np.float32)]
+    got = gpu_engine.extract_host(clips)
+    assert [len(g) for g in got] == [0, 0, 0]
+
+
+def test_long_track_multi_chunk(gpu_engine):
+    # 3 K3 chunks (1024 anchor frames each) and many K2 strips
+    x = _clip(99, 2048 + 512 * 2600, start=5)
+    got = gpu_engine.extract_host([x])[0]
+    ref = O.fingerprint(x, HOP)
+    assert len(ref) > 1000
+    assert np.array_equal(got, ref)
+
+
+def test_batch_256_full_config(gpu_engine):
+    """BASELINE config 2 shape: 256 x 10 s, device-resident PCM, every clip bit-exact."""
+    import torch
+
+    n = 441000
+    tracks = np.arange(1000, 1256, dtype=np.uint32)
+    pcm = torch.empty(256 * n, dtype=torch.float32, device="cuda")
+    gpu_engine.synth(pcm.data_ptr(), tracks, np.zeros(256, np.int64), n)
+    host = pcm.cpu().numpy().reshape(256, n)
+    # generator parity on a few clips
+    for c in (0, 17, 255):
+        assert np.array_equal(host[c], synth.synth(int(tracks[c]), 0, n, SR))
+    offs = np.arange(257, dtype=np.int64) * n
+    gpu_engine.extract_device(pcm.data_ptr(), offs)
+    counts = gpu_engine.counts()
+    ref = O.fingerprint_batch(host, HOP, threads=16)
+    for c in range(256):
+        assert counts[c] == len(ref[c])
+        assert np.array_equal(gpu_engine.hashes(c), ref[c]), f"clip {c}"
+
+
+def test_logmag_tolerance(gpu_engine):
+    """STFT magnitudes within 1e-4 rel (frame-normalised), log-mag within 60 dB of the peak."""
+    x = _clip(3, 220500, snr=20)
+    L = gpu_engine.spectrogram(x).astype(np.float64)
+    P64 = O.stft_power_f64(x, HOP)
+    L64 = 10 * np.log10(P64 + 1e-10)
+    m = np.sqrt(np.maximum(10 ** (L / 10) - 1e-10, 0))
+    m64 = np.sqrt(P64)
+    assert (np.abs(m - m64) / m64.max(axis=1, keepdims=True)).max() <= 1e-4
+    sel = P64 >= 1e-6 * P64.max(axis=1, keepdims=True)
+    assert np.abs(L - L64)[sel].max() <= 1e-4 * 60.0
