@@ -168,10 +168,14 @@ class Engine:
 
 
 def peaks_from_mask(mask: np.ndarray) -> np.ndarray:
-    """[F,16] uint64 bitmask -> [n,2] int32 (t, k) in (t, k) order."""
+    """[F,16] uint64 K2 mask -> [n,2] int32 (t, k) in (t, k) order.
+
+    K2's ballot layout: word 4*w + i, bit l = peak flag of bin 256*w + 4*l + i."""
     F = mask.shape[0]
     bits = np.unpackbits(mask.astype("<u8").view(np.uint8).reshape(F, 16, 8), axis=2, bitorder="little")
-    t, k = np.nonzero(bits.reshape(F, 1024))
+    bits = bits.reshape(F, 4, 4, 64)  # [F][w][i][l]
+    nat = bits.transpose(0, 1, 3, 2).reshape(F, 1024)  # bin = 256w + 4l + i
+    t, k = np.nonzero(nat)
     return np.stack([t, k], axis=1).astype(np.int32)
 
 

@@ -13,10 +13,9 @@ constexpr int kZoneDF = 127;      // target zone, bins
 constexpr int kFan = 10;          // targets per anchor
 constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 
-// K1: frames per workgroup (4 waves x kStftFramesPerWave)
-constexpr int kStftWaves = 4;
-constexpr int kStftFramesPerWave = 16;
-constexpr int kStftFramesPerBlock = kStftWaves * kStftFramesPerWave;
+// K1: 12 waves per workgroup, each wave slides over a strip of kStftStrip frames
+constexpr int kStftWaves = 12;
+constexpr int kStftStrip = 16;
 constexpr int kStftLdsPerWave = 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024+32)
 
 // K2: output frames per workgroup strip
@@ -39,7 +38,7 @@ struct ClipDesc {
     int64_t chunk_base;  // first K3 chunk of the clip
     int64_t hash_base;   // first record slot of the clip in the output buffer
     int64_t hash_cap;    // record capacity of the clip
-    int64_t reserved;
+    int64_t stft_base;   // first K1 wave-strip of the clip
 };
 
 }  // namespace aid

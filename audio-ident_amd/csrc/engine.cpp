@@ -19,7 +19,7 @@
 #include "aidfp_layout.h"
 
 namespace aid {
-void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames, int hop,
+void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_strips, int hop,
                        const Tables *tab, float *out, bool logmag, hipStream_t s);
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, float thr,
                       uint64_t *mask, hipStream_t s);
@@ -180,7 +180,8 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     aid_config c = *cfg;
     if (c.sample_rate <= 0) return fail(AID_ERR_INVALID, "sample_rate must be > 0");
     if (c.hop == 0) c.hop = c.sample_rate >= 32000 ? 512 : 256;
-    if (c.hop < 128 || c.hop % 128 != 0 || c.hop > 2048) return fail(AID_ERR_INVALID, "hop must be a multiple of 128 in [128, 2048]");
+    if (c.hop != 128 && c.hop != 256 && c.hop != 512 && c.hop != 1024 && c.hop != 2048)
+        return fail(AID_ERR_INVALID, "hop must be one of 128, 256, 512, 1024, 2048");
     if (c.peak_threshold == 0.0f) c.peak_threshold = 4.0f;
     if (!(c.peak_threshold > 0.0f)) return fail(AID_ERR_INVALID, "peak_threshold must be > 0");
     if (c.min_match <= 0) c.min_match = 5;
@@ -283,7 +284,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     e->clip_base.assign(n_clips, 0);
     e->clip_frames.assign(n_clips, 0);
-    int64_t frames = 0, strips = 0, chunks = 0, recs = 0, staged = 0;
+    int64_t frames = 0, strips = 0, chunks = 0, recs = 0, staged = 0, kstrips = 0;
     for (int c = 0; c < n_clips; ++c) {
         const int64_t n = offsets[c + 1] - offsets[c];
         const int64_t F = num_frames(n, hop);
@@ -301,13 +302,14 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         d.chunk_base = chunks;
         d.hash_base = recs;
         d.hash_cap = hash_capacity(F);
-        d.reserved = 0;
+        d.stft_base = kstrips;
         e->clip_base[c] = recs;
         e->clip_frames[c] = F;
         frames += F;
         strips += (F + kPeakStrip - 1) / kPeakStrip;
         chunks += (F + kHashChunk - 1) / kHashChunk;
         recs += d.hash_cap;
+        kstrips += (F + kStftStrip - 1) / kStftStrip;
     }
     HIP_TRY(e->desc.reserve((size_t)n_clips + 1));
     HIP_TRY(e->power.reserve((size_t)frames * kBins));
@@ -337,7 +339,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
     if (frames > 0) {
         {
             ProfScope ps(e, AID_K_STFT, s);
-            launch_stft_power(dpcm, e->desc.p, n_clips, frames, hop, e->d_tab, e->power.p, false, s);
+            launch_stft_power(dpcm, e->desc.p, n_clips, kstrips, hop, e->d_tab, e->power.p, false, s);
         }
         {
             ProfScope ps(e, AID_K_PEAKS, s);
@@ -451,7 +453,7 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_pcm, pcm, n * sizeof(float), hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
-        launch_stft_power(d_pcm, d_desc, 1, F, e->cfg.hop, e->d_tab, d_out, true, s);
+        launch_stft_power(d_pcm, d_desc, 1, (F + kStftStrip - 1) / kStftStrip, e->cfg.hop, e->d_tab, d_out, true, s);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);

@@ -37,6 +37,24 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[25
     return incl - v;
 }
 
+// bit l of x (l < 16) -> bit 4l
+__device__ __forceinline__ uint64_t spread4(uint64_t x) {
+    x &= 0xFFFFull;
+    x = (x | (x << 24)) & 0x000000FF000000FFull;
+    x = (x | (x << 12)) & 0x000F000F000F000Full;
+    x = (x | (x << 6)) & 0x0303030303030303ull;
+    x = (x | (x << 3)) & 0x1111111111111111ull;
+    return x;
+}
+
+// K2 stores word 4*w + i = ballot over lanes l of bin 256*w + 4*l + i; natural word
+// n (bins 64n .. 64n+63) takes lanes 16*(n&3) .. +15 of the four words of block n>>2.
+__device__ __forceinline__ uint64_t natural_word(const uint64_t (&W)[kMaskWords], int n) {
+    const int blk = 4 * (n >> 2), sh = 16 * (n & 3);
+    return spread4(W[blk + 0] >> sh) | (spread4(W[blk + 1] >> sh) << 1) | (spread4(W[blk + 2] >> sh) << 2) |
+           (spread4(W[blk + 3] >> sh) << 3);
+}
+
 __device__ __forceinline__ uint32_t make_hash(int k1, int k2, int dt) {
     return ((uint32_t)(k1 & 0x3FF) << 22) | ((uint32_t)(k2 & 0x3FF) << 12) | ((uint32_t)dt & 0xFFF);
 }
@@ -78,12 +96,15 @@ __global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ 
     }
     int64_t npk = 0;
     int64_t run = block_excl_scan(mine, scan_tmp, &npk);
-    // 2. expand to the (t,k)-ordered peak list
+    // 2. expand to the (t,k)-ordered peak list (unshuffling K2's ballot layout)
     for (int f = fa; f < fz; ++f) {
         const uint32_t c = foff[f];
         int64_t idx = run;
+        uint64_t W[kMaskWords];
+#pragma unroll
+        for (int w = 0; w < kMaskWords; ++w) W[w] = Mc[f * kMaskWords + w];
         for (int w = 0; w < kMaskWords; ++w) {
-            uint64_t m = Mc[f * kMaskWords + w];
+            uint64_t m = natural_word(W, w);
             while (m) {
                 const int bpos = __ffsll((unsigned long long)m) - 1;
                 plist[idx++] = ((uint32_t)f << 10) | (uint32_t)(64 * w + bpos);

@@ -6,133 +6,162 @@
 // :185-193 query).
 //
 // Work mapping (gfx950, wave64):
-//   * a workgroup = 4 waves; the 4 waves take 4 consecutive frames at a time so
-//     their 75 %-overlapping PCM loads share the CU's L1 (HBM reads PCM ~once);
-//   * lane l loads z[64*n1 + l] (n1 < 16) as float2: 512 contiguous bytes per
-//     wave-instruction;
-//   * stage A = 16-point DFT in registers, twiddle, LDS transpose (E1, row stride
-//     68 float2: conflict-free for both the write and the strided read);
+//   * each wave owns a strip of kStftStrip consecutive frames of one clip. Lane l
+//     keeps the complex samples z[64*n1 + l] (n1 < 16, "rows" of 128 PCM samples)
+//     in a 16-slot register ring: frame t+1 reuses 16 - H/128 rows of frame t, so
+//     only the new hop is loaded (H/128 float2 loads per lane, 512 contiguous bytes
+//     per wave-instruction) and every PCM byte crosses HBM -> VGPR once per strip;
+//     the next frame's rows are loaded right after the window multiply so their
+//     latency hides under the FFT;
+//   * stage A = 16-point DFT in registers, twiddle (LDS table laid out [k1][lane]),
+//     LDS transpose (E1, row stride 68 float2: conflict-free write and read);
 //   * stage B = 16-point DFT in registers, twiddle, quad exchange through LDS
 //     (E2, lane stride 17 float2);
 //   * stage C = radix-4 in registers, natural-order spill to LDS (E3, +1 pad per
 //     32), then the real split reads Z[k] and Z[1024-k] (both conflict-free) and
 //     stores 64 consecutive bins per wave-instruction.
-// The exchanges are wave-private, so there is no workgroup barrier in the loop.
+// A workgroup is 12 waves (3 per SIMD) sharing 24.5 KB of tables in LDS; the
+// exchanges are wave-private, so there is no workgroup barrier in the loop.
 #include "aidfp_device.h"
 
 namespace aid {
 
-__device__ __forceinline__ int find_clip_by_frame(const ClipDesc *__restrict__ clips, int n_clips, int64_t g) {
-    int lo = 0, hi = n_clips - 1;
-    while (lo < hi) {  // last clip with frame_base <= g (wave-uniform: scalar loads)
-        int mid = (lo + hi + 1) >> 1;
-        if (clips[mid].frame_base <= g) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-template <bool LOGMAG>
-__global__ __launch_bounds__(256, 3) void k_stft_power(const float *__restrict__ pcm, const ClipDesc *__restrict__ clips,
-                                                   int n_clips, int64_t total_frames, int hop,
-                                                   const Tables *__restrict__ tab, float *__restrict__ out) {
+template <bool LOGMAG, int ROWS>
+__global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
+                                                                const ClipDesc *__restrict__ clips, int n_clips,
+                                                                int64_t total_strips, const Tables *__restrict__ tab,
+                                                                float *__restrict__ out) {
+    constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
+    constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ float2 lds[kStftWaves][kStftLdsPerWave];
-    __shared__ float2 s_win[1024], s_t2k[1024], s_t64[64];
+    __shared__ float2 s_win[1024], s_ta[1024], s_t2k[1024], s_t64[64];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     float2 *buf = lds[wave];
     const int kq = lane >> 2;  // stage B/C: k1
     const int mq = lane & 3;   // stage B: m2 ; stage C: s
 
-    // window, T2K, T64 staged once per workgroup (LDS reads are 4x cheaper than L1 here)
-    for (int i = threadIdx.x; i < 1024; i += 256) {
+    for (int i = threadIdx.x; i < 1024; i += kStftWaves * 64) {
         s_win[i] = tab->win2[i];
         s_t2k[i] = tab->t2k[i];
+        const int k1 = i >> 6, l = i & 63;
+        s_ta[i] = tab->t1k[l * k1];  // [k1][lane] = T1K[lane*k1]
     }
     if (threadIdx.x < 64) s_t64[threadIdx.x] = tab->t64[threadIdx.x];
-    float2 twA[16], t16[10];
+    float2 t16[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) t16[i] = tab->t16[i];
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) twA[k1] = tab->t1k[lane * k1];
     __syncthreads();
 
-    for (int f = 0; f < kStftFramesPerWave; ++f) {
-        const int64_t g = (int64_t)blockIdx.x * kStftFramesPerBlock + f * kStftWaves + wave;
-        if (g >= total_frames) break;  // wave-uniform
-        const int c = find_clip_by_frame(clips, n_clips, g);
-        const int64_t t = g - clips[c].frame_base;
-        const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[c].pcm_off + t * hop);
+    const int64_t strip = (int64_t)blockIdx.x * kStftWaves + wave;
+    if (strip >= total_strips) return;  // wave-uniform, after the only barrier
+    int lo = 0, hi = n_clips - 1;
+    while (lo < hi) {  // last clip with stft_base <= strip (scalar loads)
+        const int mid = (lo + hi + 1) >> 1;
+        if (clips[mid].stft_base <= strip) lo = mid; else hi = mid - 1;
+    }
+    const int64_t t0 = (strip - clips[lo].stft_base) * kStftStrip;
+    const int nfr = (int)min((int64_t)kStftStrip, clips[lo].frames - t0);
+    const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + lane;
+    float *dst = out + (clips[lo].frame_base + t0) * kBins;
 
-        float2 v[16];
+    float2 ring[16];
 #pragma unroll
-        for (int n1 = 0; n1 < 16; ++n1) {
-            const float2 x = src[64 * n1 + lane];
-            const float2 w = s_win[64 * n1 + lane];
-            v[n1] = make_float2(x.x * w.x, x.y * w.y);
-        }
-        // stage A: lane = n2
-        dft16(v, t16);
-        // T1K[n2*k1]; lane 0 multiplies by T1K[0] = (1,-0): value-identical (FPSPEC 4 note)
+    for (int r = 0; r < 16; ++r) ring[r] = src[64 * r];
+
+    for (int f0 = 0; f0 < nfr; f0 += PERIOD) {
 #pragma unroll
-        for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], twA[k1]);
-        // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
+        for (int p = 0; p < PERIOD; ++p) {
+            const int f = f0 + p;
+            if (f < nfr) {  // wave-uniform
+                float2 v[16];
 #pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 68 + lane] = v[k1];
-        wave_lds_sync();
+                for (int n1 = 0; n1 < 16; ++n1) {
+                    const float2 x = ring[(n1 + ROWS * p) & 15];
+                    const float2 w = s_win[64 * n1 + lane];
+                    v[n1] = make_float2(x.x * w.x, x.y * w.y);
+                }
+                // the rows just consumed (n1 < ROWS) are replaced by frame f+1's new rows
+                if (f + 1 < nfr) {
 #pragma unroll
-        for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[kq * 68 + 4 * m1 + mq];
-        wave_lds_sync();
-        // stage B
-        dft16(v, t16);
+                    for (int j = 0; j < ROWS; ++j)
+                        ring[(ROWS * p + j) & 15] = src[(int64_t)(f + 1) * HOP2 + 64 * (16 - ROWS + j)];
+                }
+                // stage A: lane = n2
+                dft16(v, t16);
+                // T1K[n2*k1]; lane 0 multiplies by T1K[0] = (1,-0): value-identical (FPSPEC 4 note)
 #pragma unroll
-        for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], s_t64[mq * j1]);
-        // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
+                for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], s_ta[64 * k1 + lane]);
+                // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
 #pragma unroll
-        for (int j1 = 0; j1 < 16; ++j1) buf[lane * 17 + j1] = v[j1];
-        wave_lds_sync();
+                for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 68 + lane] = v[k1];
+                wave_lds_sync();
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+                for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[kq * 68 + 4 * m1 + mq];
+                wave_lds_sync();
+                // stage B
+                dft16(v, t16);
 #pragma unroll
-            for (int m2 = 0; m2 < 4; ++m2) v[4 * r + m2] = buf[(4 * kq + m2) * 17 + mq + 4 * r];
-        wave_lds_sync();
-        // stage C: DFT4 over m2 -> Z[kq + 16*(mq + 4r) + 256*j2]; E3 natural order, pad 1 per 32
+                for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], s_t64[mq * j1]);
+                // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            dft4(v[4 * r + 0], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+                for (int j1 = 0; j1 < 16; ++j1) buf[lane * 17 + j1] = v[j1];
+                wave_lds_sync();
 #pragma unroll
-            for (int j2 = 0; j2 < 4; ++j2) {
-                const int k = kq + 16 * (mq + 4 * r) + 256 * j2;
-                buf[k + (k >> 5)] = v[4 * r + j2];
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int m2 = 0; m2 < 4; ++m2) v[4 * r + m2] = buf[(4 * kq + m2) * 17 + mq + 4 * r];
+                wave_lds_sync();
+                // stage C: DFT4 over m2 -> Z[kq + 16*(mq + 4r) + 256*j2]; E3 natural order, pad 1 per 32
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    dft4(v[4 * r + 0], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
+#pragma unroll
+                    for (int j2 = 0; j2 < 4; ++j2) {
+                        const int k = kq + 16 * (mq + 4 * r) + 256 * j2;
+                        buf[k + (k >> 5)] = v[4 * r + j2];
+                    }
+                }
+                wave_lds_sync();
+                float *drow = dst + (int64_t)f * kBins;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int k = lane + 64 * i;
+                    const int kk = (1024 - k) & 1023;
+                    const float2 a = buf[k + (k >> 5)];
+                    const float2 b = buf[kk + (kk >> 5)];
+                    const float2 o = make_float2(a.y + b.y, b.x - a.x);
+                    const float er = a.x + b.x, ei = a.y - b.y;
+                    const float2 tw = cmul(o, s_t2k[k]);
+                    const float xr = er + tw.x, xi = ei + tw.y;
+                    const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                    if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
+                    else drow[k] = P;
+                }
+                wave_lds_sync();
             }
         }
-        wave_lds_sync();
-        float *dst = out + g * kBins;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int k = lane + 64 * i;
-            const int kk = (1024 - k) & 1023;
-            const float2 p = buf[k + (k >> 5)];
-            const float2 q = buf[kk + (kk >> 5)];
-            const float2 o = make_float2(p.y + q.y, q.x - p.x);
-            const float er = p.x + q.x, ei = p.y - q.y;
-            const float2 tw = cmul(o, s_t2k[k]);
-            const float xr = er + tw.x, xi = ei + tw.y;
-            const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
-            if constexpr (LOGMAG) dst[k] = 10.0f * log10f(P + 1e-10f);
-            else dst[k] = P;
-        }
-        wave_lds_sync();
     }
 }
 
-void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames, int hop,
+template <bool LOGMAG>
+static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
+                        int64_t total_strips, const Tables *tab, float *out) {
+    switch (rows) {
+        case 1: hipLaunchKernelGGL((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
+        case 2: hipLaunchKernelGGL((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
+        case 4: hipLaunchKernelGGL((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
+        case 8: hipLaunchKernelGGL((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
+        default: hipLaunchKernelGGL((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
+    }
+}
+
+void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_strips, int hop,
                        const Tables *tab, float *out, bool logmag, hipStream_t s) {
-    if (total_frames <= 0) return;
-    const unsigned blocks = (unsigned)((total_frames + kStftFramesPerBlock - 1) / kStftFramesPerBlock);
-    if (logmag)
-        hipLaunchKernelGGL(k_stft_power<true>, dim3(blocks), dim3(256), 0, s, pcm, clips, n_clips, total_frames, hop, tab, out);
-    else
-        hipLaunchKernelGGL(k_stft_power<false>, dim3(blocks), dim3(256), 0, s, pcm, clips, n_clips, total_frames, hop, tab, out);
+    if (total_strips <= 0) return;
+    const dim3 g((unsigned)((total_strips + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
+    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total_strips, tab, out);
+    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total_strips, tab, out);
 }
 
 }  // namespace aid
