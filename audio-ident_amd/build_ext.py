@@ -37,32 +37,37 @@ def _deps(src: Path) -> list[Path]:
     return [src] + sorted(CSRC.glob("*.h")) + [PKG.parent / "include" / "aidfp.h"]
 
 
-def _compile(name: str, verbose: bool) -> Path:
+def _compile(name: str, verbose: bool, objdir: Path = OBJ, extra: tuple = ()) -> Path:
     src = CSRC / name
-    obj = OBJ / (name + ".o")
+    obj = objdir / (name + ".o")
     if obj.exists() and all(d.stat().st_mtime <= obj.stat().st_mtime for d in _deps(src)):
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *FLAGS, *extra, "-c", str(src), "-o", str(obj)]
     if name.endswith(".cpp"):
-        cmd = [HIPCC, *FLAGS, "-x", "hip", "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *FLAGS, *extra, "-x", "hip", "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     return obj
 
 
-def build(verbose: bool = False) -> Path:
-    OBJ.mkdir(exist_ok=True)
+def build(verbose: bool = False, variant: str | None = None, defines: tuple = ()) -> Path:
+    """Build the product library; `variant` builds a diagnostic copy (build/<variant>/libaidfp.so)
+    with extra -D defines, used only for profiling experiments (never loaded by default)."""
+    objdir = OBJ if variant is None else OBJ / variant
+    lib = LIB if variant is None else objdir / "libaidfp.so"
+    objdir.mkdir(parents=True, exist_ok=True)
+    extra = tuple(f"-D{d}" for d in defines)
     srcs = [s for s in SOURCES if (CSRC / s).exists()]
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, verbose), srcs))
-    if LIB.exists() and all(o.stat().st_mtime <= LIB.stat().st_mtime for o in objs):
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+        objs = list(ex.map(lambda s: _compile(s, verbose, objdir, extra), srcs))
+    if lib.exists() and all(o.stat().st_mtime <= lib.stat().st_mtime for o in objs):
+        return lib
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

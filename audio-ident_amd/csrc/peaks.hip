@@ -108,6 +108,9 @@ __global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ pow
                 const float4 w = reinterpret_cast<const float4 *>(rb)[tid + v];
                 q[4 * v + 0] = w.x; q[4 * v + 1] = w.y; q[4 * v + 2] = w.z; q[4 * v + 3] = w.w;
             }
+            // keep the two unused edge floats live: otherwise hipcc re-pairs the used floats into
+            // ds_read2_b32 at a 16-byte lane stride (8-way bank conflict) instead of 9 ds_read_b128
+            asm volatile("" ::"v"(q[0]), "v"(q[35]));
             // own bin i is q[16+i]; left window q[1+i..15+i], right window q[17+i..31+i]
             float midL = q[4], midR = q[20];
 #pragma unroll

@@ -17,14 +17,27 @@
 //     LDS transpose (E1, row stride 68 float2: conflict-free write and read);
 //   * stage B = 16-point DFT in registers, twiddle, quad exchange through LDS
 //     (E2, lane stride 17 float2);
-//   * stage C = radix-4 in registers, natural-order spill to LDS (E3, +1 pad per
-//     32), then the real split reads Z[k] and Z[1024-k] (both conflict-free) and
+//   * stage C = radix-4 in registers, spill to LDS in XOR-swizzled natural order
+//     (E3), then the real split reads Z[k] and Z[1024-k] (both conflict-free) and
 //     stores 64 consecutive bins per wave-instruction.
-// A workgroup is 12 waves (3 per SIMD) sharing 24.5 KB of tables in LDS; the
+// A workgroup is 12 waves (3 per SIMD) sharing 32 KB of tables in LDS; the
 // exchanges are wave-private, so there is no workgroup barrier in the loop.
 #include "aidfp_device.h"
 
+// AID_K1_DIAG selects a timing-only variant for LDS-conflict attribution (wrong results):
+//   1 = E3 writes lane-contiguous, 2 = real-split mirror reads lane-contiguous,
+//   4 = E1 read lane-contiguous, 5 = E2 read lane-contiguous
+#ifndef AID_K1_DIAG
+#define AID_K1_DIAG 0
+#endif
+
 namespace aid {
+
+// E3 slot of Z[k]: XOR-swizzle bits 2-3 by bits 4-5. The stage-C writers of one 16-lane
+// group hold k = kq + 16*mq (+const): k ^ (mq << 2) puts them on 16 distinct 8-byte bank
+// pairs; the readers (k = lane + 64i, and the mirror 1024-k) stay a permutation of one or two
+// 16-entry blocks, so every access is conflict-free (the mirror read: one 2-way pair per wave).
+__device__ __forceinline__ int e3(int k) { return k ^ (((k >> 4) & 3) << 2); }
 
 template <bool LOGMAG, int ROWS>
 __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
@@ -33,8 +46,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                                                 float *__restrict__ out) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
-    __shared__ float2 lds[kStftWaves][kStftLdsPerWave];
-    __shared__ float2 s_win[1024], s_ta[1024], s_t2k[1024], s_t64[64];
+    __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68, E2: 64 x 17, E3: 1024
+    __shared__ float2 s_win[1024], s_ta[1024], s_t2k[1024], s_tb[1024];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     float2 *buf = lds[wave];
@@ -45,9 +58,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
         s_win[i] = tab->win2[i];
         s_t2k[i] = tab->t2k[i];
         const int k1 = i >> 6, l = i & 63;
-        s_ta[i] = tab->t1k[l * k1];  // [k1][lane] = T1K[lane*k1]
+        s_ta[i] = tab->t1k[l * k1];          // [k1][lane] = T1K[lane*k1]
+        s_tb[i] = tab->t64[(l & 3) * k1];    // [j1][lane] = T64[m2*j1], m2 = lane & 3
     }
-    if (threadIdx.x < 64) s_t64[threadIdx.x] = tab->t64[threadIdx.x];
     float2 t16[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) t16[i] = tab->t16[i];
@@ -97,12 +110,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 68 + lane] = v[k1];
                 wave_lds_sync();
 #pragma unroll
-                for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[kq * 68 + 4 * m1 + mq];
+                for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[AID_K1_DIAG == 4 ? m1 * 68 + lane : kq * 68 + 4 * m1 + mq];
                 wave_lds_sync();
                 // stage B
                 dft16(v, t16);
 #pragma unroll
-                for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], s_t64[mq * j1]);
+                for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], s_tb[64 * j1 + lane]);
                 // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
 #pragma unroll
                 for (int j1 = 0; j1 < 16; ++j1) buf[lane * 17 + j1] = v[j1];
@@ -110,7 +123,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
-                    for (int m2 = 0; m2 < 4; ++m2) v[4 * r + m2] = buf[(4 * kq + m2) * 17 + mq + 4 * r];
+                    for (int m2 = 0; m2 < 4; ++m2)
+                        v[4 * r + m2] = buf[AID_K1_DIAG == 5 ? (4 * r + m2) * 68 + lane : (4 * kq + m2) * 17 + mq + 4 * r];
                 wave_lds_sync();
                 // stage C: DFT4 over m2 -> Z[kq + 16*(mq + 4r) + 256*j2]; E3 natural order, pad 1 per 32
 #pragma unroll
@@ -118,8 +132,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     dft4(v[4 * r + 0], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
 #pragma unroll
                     for (int j2 = 0; j2 < 4; ++j2) {
-                        const int k = kq + 16 * (mq + 4 * r) + 256 * j2;
-                        buf[k + (k >> 5)] = v[4 * r + j2];
+                        const int k = AID_K1_DIAG == 1 ? lane + 64 * (r + 4 * j2) : kq + 16 * (mq + 4 * r) + 256 * j2;
+                        buf[e3(k)] = v[4 * r + j2];
                     }
                 }
                 wave_lds_sync();
@@ -127,9 +141,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int k = lane + 64 * i;
-                    const int kk = (1024 - k) & 1023;
-                    const float2 a = buf[k + (k >> 5)];
-                    const float2 b = buf[kk + (kk >> 5)];
+                    const int kk = AID_K1_DIAG == 2 ? (k ^ 512) : (1024 - k) & 1023;
+                    const float2 a = buf[e3(k)];
+                    const float2 b = buf[e3(kk)];
                     const float2 o = make_float2(a.y + b.y, b.x - a.x);
                     const float er = a.x + b.x, ei = a.y - b.y;
                     const float2 tw = cmul(o, s_t2k[k]);
