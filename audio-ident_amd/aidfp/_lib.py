@@ -19,9 +19,9 @@ AID_ERR_NOMEM = -3
 AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
-AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH = range(5)
-AID_K_COUNT = 5
-KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth"]
+AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
+AID_K_COUNT = 6
+KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match"]
 
 
 class EngineUnavailable(RuntimeError):
@@ -50,6 +50,16 @@ class AidHash(ctypes.Structure):
     _fields_ = [("hash", ctypes.c_uint32), ("t1", ctypes.c_uint32)]
 
 
+class AidMatchRow(ctypes.Structure):
+    _fields_ = [
+        ("match_count", ctypes.c_int32),
+        ("track", ctypes.c_uint32),
+        ("d", ctypes.c_int32),
+        ("tq_min", ctypes.c_int32),
+        ("tq_max", ctypes.c_int32),
+    ]
+
+
 # (name, restype, argtypes) for every symbol include/aidfp.h declares
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
@@ -72,6 +82,17 @@ SIGNATURES = [
     ("aid_result_peakmask", ctypes.c_int, [P, I32, P, I64]),
     ("aid_spectrogram", ctypes.c_int, [P, P, I64, P, I64]),
     ("aid_synth", ctypes.c_int, [P, P, P, P, I32, I64, I32, ctypes.c_uint32, P]),
+    ("aid_index_reset", ctypes.c_int, [P]),
+    ("aid_index_add_extracted", ctypes.c_int, [P, P]),
+    ("aid_index_add_postings", ctypes.c_int, [P, P, P, P, I64, I32]),
+    ("aid_index_remove", ctypes.c_int, [P, ctypes.c_uint32]),
+    ("aid_index_finalize", ctypes.c_int, [P]),
+    ("aid_index_stats", ctypes.c_int, [P, P, P, P]),
+    ("aid_index_export", ctypes.c_int, [P, P, P, P, I64, I64, I32]),
+    ("aid_index_save", ctypes.c_int, [P, ctypes.c_char_p]),
+    ("aid_index_load", ctypes.c_int, [P, ctypes.c_char_p]),
+    ("aid_query", ctypes.c_int, [P, P, P, I32, P, P]),
+    ("aid_query_extracted", ctypes.c_int, [P, P, P]),
     ("aid_profile_enable", ctypes.c_int, [P, I32]),
     ("aid_profile_read", ctypes.c_int, [P, P, P, I32]),
 ]

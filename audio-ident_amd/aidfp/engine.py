@@ -13,7 +13,8 @@ from typing import Sequence
 import numpy as np
 
 from . import _lib as L
-from ._lib import AID_ERR_DEVICE, AID_PCM_DEVICE, AID_PCM_HOST, AidConfig, EngineError, EngineUnavailable, check
+from ._lib import (AID_ERR_DEVICE, AID_PCM_DEVICE, AID_PCM_HOST, AidConfig, AidMatchRow, EngineError,
+                   EngineUnavailable, check)
 
 N_FFT = 2048
 BINS = 1024
@@ -155,6 +156,88 @@ class Engine:
         st = np.ascontiguousarray(starts, dtype=np.int64)
         check(self._lib.aid_synth(self._h, ctypes.c_void_p(dst_ptr), _p(tr), _p(st), len(tr), int(n), int(noise_a),
                                   int(salt) & 0xFFFFFFFF, ctypes.c_void_p(stream) if stream else None))
+
+    # -- index + match (FPSPEC 7) --
+    def index_reset(self) -> None:
+        check(self._lib.aid_index_reset(self._h))
+
+    def index_add_extracted(self, track_ids) -> None:
+        """Index every clip of the last extraction under track_ids[c]."""
+        tr = np.ascontiguousarray(track_ids, dtype=np.uint32)
+        if len(tr) != self.n_clips:
+            raise ValueError("one track id per extracted clip")
+        check(self._lib.aid_index_add_extracted(self._h, _p(tr)))
+
+    def index_add_records(self, track: int, records: np.ndarray) -> None:
+        """Index host records (uint64 hash | t1 << 32) as track `track`."""
+        rec = np.ascontiguousarray(records, dtype=np.uint64)
+        h = np.ascontiguousarray((rec & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+        t = np.ascontiguousarray((rec >> np.uint64(32)).astype(np.uint32))
+        tr = np.full(len(rec), track, dtype=np.uint32)
+        check(self._lib.aid_index_add_postings(self._h, _p(h), _p(tr), _p(t), len(rec), AID_PCM_HOST))
+
+    def index_add_postings(self, hash_ptr: int, track_ptr: int, t_ptr: int, n: int, device: bool = True) -> None:
+        check(self._lib.aid_index_add_postings(self._h, ctypes.c_void_p(hash_ptr), ctypes.c_void_p(track_ptr),
+                                               ctypes.c_void_p(t_ptr), int(n), AID_PCM_DEVICE if device else AID_PCM_HOST))
+
+    def index_remove(self, track: int) -> None:
+        check(self._lib.aid_index_remove(self._h, int(track)))
+
+    def index_finalize(self) -> None:
+        check(self._lib.aid_index_finalize(self._h))
+
+    def index_stats(self) -> dict:
+        n = ctypes.c_int64()
+        live = ctypes.c_int64()
+        nt = ctypes.c_uint32()
+        check(self._lib.aid_index_stats(self._h, ctypes.byref(n), ctypes.byref(live), ctypes.byref(nt)))
+        return {"postings": n.value, "live": live.value, "tracks": nt.value}
+
+    def index_export(self, first: int = 0, count: int | None = None) -> np.ndarray:
+        """Host copy of stored postings [first, first+count) as [n, 3] uint32 (hash, track, t)."""
+        total = self.index_stats()["postings"]
+        count = total - first if count is None else count
+        cols = [np.zeros(max(count, 1), dtype=np.uint32) for _ in range(3)]
+        check(self._lib.aid_index_export(self._h, _p(cols[0]), _p(cols[1]), _p(cols[2]), first, count, AID_PCM_HOST))
+        return np.stack([c[:count] for c in cols], axis=1)
+
+    def index_export_device(self, hash_ptr: int, track_ptr: int, t_ptr: int, first: int, count: int) -> None:
+        check(self._lib.aid_index_export(self._h, ctypes.c_void_p(hash_ptr), ctypes.c_void_p(track_ptr),
+                                         ctypes.c_void_p(t_ptr), first, count, AID_PCM_DEVICE))
+
+    def index_save(self, path: str) -> None:
+        check(self._lib.aid_index_save(self._h, str(path).encode()))
+
+    def index_load(self, path: str) -> None:
+        check(self._lib.aid_index_load(self._h, str(path).encode()))
+
+    def _rows(self, rows, nrows, nq: int) -> list[np.ndarray]:
+        arr = np.ctypeslib.as_array(rows).view(np.int32).reshape(nq, self.max_results, 5)
+        return [arr[q, : nrows[q]].astype(np.int64) for q in range(nq)]
+
+    def query(self, queries) -> list[np.ndarray]:
+        """Match host record arrays; per query [r, 5] int64 rows (count, track, d, tq_min, tq_max)."""
+        qs = [np.ascontiguousarray(q, dtype=np.uint64).ravel() for q in queries]
+        nq = len(qs)
+        if nq == 0:
+            return []
+        qoff = np.zeros(nq + 1, dtype=np.int64)
+        qoff[1:] = np.cumsum([len(q) for q in qs])
+        recs = np.concatenate(qs) if qoff[-1] else np.zeros(1, dtype=np.uint64)
+        rows = (AidMatchRow * (nq * self.max_results))()
+        nrows = np.zeros(nq, dtype=np.int32)
+        check(self._lib.aid_query(self._h, _p(recs), _p(qoff), nq, ctypes.addressof(rows), _p(nrows)))
+        return self._rows(rows, nrows, nq)
+
+    def query_extracted(self) -> list[np.ndarray]:
+        """Match every clip of the last extraction (records never leave the device)."""
+        nq = self.n_clips
+        if nq == 0:
+            return []
+        rows = (AidMatchRow * (nq * self.max_results))()
+        nrows = np.zeros(nq, dtype=np.int32)
+        check(self._lib.aid_query_extracted(self._h, ctypes.addressof(rows), _p(nrows)))
+        return self._rows(rows, nrows, nq)
 
     # -- profiling --
     def profile_enable(self, on: bool = True) -> None:

@@ -27,6 +27,19 @@ void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, 
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
                   int noise_a, uint32_t salt, const int16_t *sin_tab, hipStream_t s);
+void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
+                        uint32_t *cnt, hipStream_t s);
+void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
+                          const uint8_t *tomb, uint32_t n_tracks, uint32_t *cursor, uint64_t *post, hipStream_t s);
+void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
+void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
+                                const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
+                                uint32_t *ptrack, uint32_t *pt, hipStream_t s);
+void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
+                  const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
+                  uint32_t *hist, int32_t *rows, int32_t *nrows, hipStream_t s);
+uint32_t index_keys();
+uint32_t index_hist_words();
 }  // namespace aid
 
 using namespace aid;
@@ -92,6 +105,25 @@ struct aid_engine {
     DevBuf<int64_t> counts;
     DevBuf<uint32_t> synth_tracks;
     DevBuf<int64_t> synth_starts;
+
+    // index (FPSPEC 7): all postings (SoA source of truth) + the CSR built from them
+    DevBuf<uint32_t> p_hash, p_track, p_t;
+    int64_t n_post = 0;
+    std::vector<uint8_t> h_tomb;  // per track id: 1 = removed
+    DevBuf<uint8_t> tomb;
+    uint32_t n_tracks = 0;        // max track id + 1
+    DevBuf<uint32_t> idx_cnt, idx_off, scan_tmp;
+    DevBuf<uint64_t> idx_post;
+    bool index_built = false, index_dirty = true;
+    int64_t n_indexed = 0;
+    // query workspaces
+    DevBuf<uint64_t> q_recs;
+    DevBuf<int64_t> q_start, q_count;
+    DevBuf<uint32_t> q_hist;
+    DevBuf<int32_t> q_rows, q_nrows;
+    DevBuf<int64_t> x_src, x_dst;
+    DevBuf<uint32_t> x_tracks;
+    size_t hist_zero_cap = 0;  // q_hist capacity known to be all-zero
 
     ClipDesc *h_desc = nullptr;  // pinned
     size_t h_desc_cap = 0;
@@ -243,6 +275,23 @@ void aid_engine_destroy(aid_engine *e) {
     e->counts.release();
     e->synth_tracks.release();
     e->synth_starts.release();
+    e->p_hash.release();
+    e->p_track.release();
+    e->p_t.release();
+    e->tomb.release();
+    e->idx_cnt.release();
+    e->idx_off.release();
+    e->scan_tmp.release();
+    e->idx_post.release();
+    e->q_recs.release();
+    e->q_start.release();
+    e->q_count.release();
+    e->q_hist.release();
+    e->q_rows.release();
+    e->q_nrows.release();
+    e->x_src.release();
+    e->x_dst.release();
+    e->x_tracks.release();
     if (e->h_desc) (void)hipHostFree(e->h_desc);
     if (e->d_tab) (void)hipFree(e->d_tab);
     if (e->d_sin) (void)hipFree(e->d_sin);
@@ -518,6 +567,323 @@ int aid_profile_read(aid_engine *e, double *ms, int64_t *launches, int32_t reset
             e->prof_n[k] = 0;
         }
     return AID_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- index + query
+
+static int grow_copy_u32(DevBuf<uint32_t> &b, size_t keep, size_t want, hipStream_t s) {
+    if (want <= b.n) return AID_OK;
+    size_t cap = std::max(want, b.n * 2);
+    uint32_t *p = nullptr;
+    HIP_TRY(hipMalloc(&p, cap * sizeof(uint32_t)));
+    if (keep) HIP_TRY(hipMemcpyAsync(p, b.p, keep * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (b.p) (void)hipFree(b.p);
+    b.p = p;
+    b.n = cap;
+    return AID_OK;
+}
+
+static int reserve_postings(aid_engine *e, int64_t extra, hipStream_t s) {
+    const size_t want = (size_t)(e->n_post + extra);
+    if (int rc = grow_copy_u32(e->p_hash, e->n_post, want, s)) return rc;
+    if (int rc = grow_copy_u32(e->p_track, e->n_post, want, s)) return rc;
+    if (int rc = grow_copy_u32(e->p_t, e->n_post, want, s)) return rc;
+    return AID_OK;
+}
+
+static int ensure_tracks(aid_engine *e, uint32_t max_track_plus1, hipStream_t s) {
+    if (max_track_plus1 <= e->n_tracks) return AID_OK;
+    e->n_tracks = max_track_plus1;
+    e->h_tomb.resize(e->n_tracks, 0);
+    HIP_TRY(e->tomb.reserve(std::max<size_t>(e->n_tracks, 1024)));
+    HIP_TRY(hipMemcpyAsync(e->tomb.p, e->h_tomb.data(), e->n_tracks, hipMemcpyHostToDevice, s));
+    return AID_OK;
+}
+
+extern "C" {
+
+int aid_index_reset(aid_engine *e) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->n_post = 0;
+    e->n_tracks = 0;
+    e->h_tomb.clear();
+    e->index_built = false;
+    e->index_dirty = true;
+    e->n_indexed = 0;
+    return AID_OK;
+}
+
+int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids) {
+    if (!e || (!track_ids && e->n_clips > 0)) return fail(AID_ERR_INVALID, "aid_index_add_extracted: bad argument");
+    if (!e->have_result) return fail(AID_ERR_STATE, "no extraction to index");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
+    const int n = e->n_clips;
+    if (n == 0) return AID_OK;
+    std::vector<int64_t> counts(n), dst(n);
+    HIP_TRY(hipMemcpyAsync(counts.data(), e->counts.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int64_t tot = 0;
+    uint32_t mx = 0;
+    for (int c = 0; c < n; ++c) {
+        dst[c] = e->n_post + tot;
+        tot += counts[c];
+        mx = std::max(mx, track_ids[c] + 1);
+    }
+    if (int rc = reserve_postings(e, tot, s)) return rc;
+    if (int rc = ensure_tracks(e, mx, s)) return rc;
+    HIP_TRY(e->x_src.reserve(n));
+    HIP_TRY(e->x_dst.reserve(n));
+    HIP_TRY(e->x_tracks.reserve(n));
+    HIP_TRY(hipMemcpyAsync(e->x_src.p, e->clip_base.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_dst.p, dst.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_tracks.p, track_ids, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    launch_records_to_postings(e->records.p, e->x_src.p, e->counts.p, e->x_dst.p, e->x_tracks.p, n, e->p_hash.p,
+                               e->p_track.p, e->p_t.p, s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    e->n_post += tot;
+    e->index_dirty = true;
+    return AID_OK;
+}
+
+int aid_index_add_postings(aid_engine *e, const uint32_t *hash, const uint32_t *track, const uint32_t *t, int64_t n,
+                           int32_t location) {
+    if (!e || n < 0 || (n > 0 && (!hash || !track || !t))) return fail(AID_ERR_INVALID, "aid_index_add_postings: bad argument");
+    if (location != AID_PCM_HOST && location != AID_PCM_DEVICE) return fail(AID_ERR_INVALID, "bad location");
+    if (n == 0) return AID_OK;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    uint32_t mx = 0;
+    if (location == AID_PCM_HOST) {
+        for (int64_t i = 0; i < n; ++i) mx = std::max(mx, track[i] + 1);
+    } else {
+        // device track ids: one max-reduction via a host copy of the track column
+        std::vector<uint32_t> tr(n);
+        HIP_TRY(hipMemcpy(tr.data(), track, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < n; ++i) mx = std::max(mx, tr[i] + 1);
+    }
+    if (int rc = reserve_postings(e, n, s)) return rc;
+    if (int rc = ensure_tracks(e, mx, s)) return rc;
+    const hipMemcpyKind k = location == AID_PCM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(e->p_hash.p + e->n_post, hash, n * sizeof(uint32_t), k, s));
+    HIP_TRY(hipMemcpyAsync(e->p_track.p + e->n_post, track, n * sizeof(uint32_t), k, s));
+    HIP_TRY(hipMemcpyAsync(e->p_t.p + e->n_post, t, n * sizeof(uint32_t), k, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->n_post += n;
+    e->index_dirty = true;
+    return AID_OK;
+}
+
+int aid_index_remove(aid_engine *e, uint32_t track) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (track >= e->n_tracks || e->h_tomb[track]) return fail(AID_ERR_INVALID, "track not indexed");
+    HIP_TRY(hipSetDevice(e->device));
+    e->h_tomb[track] = 1;
+    HIP_TRY(hipMemcpy(e->tomb.p + track, &e->h_tomb[track], 1, hipMemcpyHostToDevice));
+    return AID_OK;
+}
+
+static int finalize_locked(aid_engine *e) {
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    if (e->n_post > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index holds more than 2^32 postings");
+    const size_t K = (size_t)index_keys() + 1;
+    HIP_TRY(e->idx_cnt.reserve(K));
+    HIP_TRY(e->idx_off.reserve(K));
+    HIP_TRY(e->scan_tmp.reserve(4 * (K / 1024 + 2) + 4096));
+    HIP_TRY(e->idx_post.reserve((size_t)std::max<int64_t>(e->n_post, 1)));
+    if (e->n_tracks == 0) HIP_TRY(e->tomb.reserve(1024));
+    HIP_TRY(hipMemsetAsync(e->idx_cnt.p, 0, K * sizeof(uint32_t), s));
+    launch_index_count(e->p_hash.p, e->p_track.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p, s);
+    launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
+    HIP_TRY(hipMemcpyAsync(e->idx_cnt.p, e->idx_off.p, K * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    launch_index_scatter(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p,
+                         e->idx_post.p, s);
+    HIP_TRY(hipGetLastError());
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, e->idx_off.p + (K - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->n_indexed = total;
+    e->index_built = true;
+    e->index_dirty = false;
+    return AID_OK;
+}
+
+int aid_index_finalize(aid_engine *e) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return finalize_locked(e);
+}
+
+int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    if (n_postings) *n_postings = e->n_post;
+    if (n_live) *n_live = e->index_built && !e->index_dirty ? e->n_indexed : -1;
+    if (n_tracks) *n_tracks = e->n_tracks;
+    return AID_OK;
+}
+
+int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t, int64_t first, int64_t count,
+                     int32_t location) {
+    if (!e || first < 0 || count < 0 || first + count > e->n_post) return fail(AID_ERR_INVALID, "aid_index_export: bad range");
+    if (count == 0) return AID_OK;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    const hipMemcpyKind k = location == AID_PCM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpy(hash, e->p_hash.p + first, count * sizeof(uint32_t), k));
+    HIP_TRY(hipMemcpy(track, e->p_track.p + first, count * sizeof(uint32_t), k));
+    HIP_TRY(hipMemcpy(t, e->p_t.p + first, count * sizeof(uint32_t), k));
+    return AID_OK;
+}
+
+static const char kIdxMagic[8] = {'A', 'I', 'D', 'F', 'P', 'I', 'X', '1'};
+
+int aid_index_save(aid_engine *e, const char *path) {
+    if (!e || !path) return fail(AID_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return fail(AID_ERR_INVALID, std::string("cannot open ") + path);
+    int64_t hdr[6] = {AID_ABI_VERSION, e->cfg.sample_rate, e->cfg.hop, e->n_post, (int64_t)e->n_tracks, 0};
+    bool ok = std::fwrite(kIdxMagic, 1, 8, f) == 8 && std::fwrite(hdr, sizeof(hdr), 1, f) == 1;
+    std::vector<uint32_t> buf((size_t)std::min<int64_t>(e->n_post, 1 << 24));
+    DevBuf<uint32_t> *cols[3] = {&e->p_hash, &e->p_track, &e->p_t};
+    for (int c = 0; c < 3 && ok; ++c)
+        for (int64_t o = 0; o < e->n_post && ok; o += (int64_t)buf.size()) {
+            const int64_t m = std::min<int64_t>((int64_t)buf.size(), e->n_post - o);
+            if (hipMemcpy(buf.data(), cols[c]->p + o, m * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) ok = false;
+            else ok = std::fwrite(buf.data(), sizeof(uint32_t), m, f) == (size_t)m;
+        }
+    if (ok && e->n_tracks) ok = std::fwrite(e->h_tomb.data(), 1, e->n_tracks, f) == e->n_tracks;
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) return fail(AID_ERR_DEVICE, std::string("failed writing ") + path);
+    return AID_OK;
+}
+
+int aid_index_load(aid_engine *e, const char *path) {
+    if (!e || !path) return fail(AID_ERR_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return fail(AID_ERR_INVALID, std::string("cannot open ") + path);
+    char magic[8];
+    int64_t hdr[6];
+    if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kIdxMagic, 8) != 0 || std::fread(hdr, sizeof(hdr), 1, f) != 1) {
+        std::fclose(f);
+        return fail(AID_ERR_INVALID, "not an aidfp index file");
+    }
+    if (hdr[1] != e->cfg.sample_rate || hdr[2] != e->cfg.hop) {
+        std::fclose(f);
+        return fail(AID_ERR_INVALID, "index sample_rate/hop differ from the engine's");
+    }
+    const int64_t n = hdr[3];
+    const uint32_t nt = (uint32_t)hdr[4];
+    hipStream_t s = e->own_stream;
+    e->n_post = 0;
+    if (int rc = reserve_postings(e, n, s)) { std::fclose(f); return rc; }
+    std::vector<uint32_t> buf((size_t)std::min<int64_t>(std::max<int64_t>(n, 1), 1 << 24));
+    DevBuf<uint32_t> *cols[3] = {&e->p_hash, &e->p_track, &e->p_t};
+    for (int c = 0; c < 3; ++c)
+        for (int64_t o = 0; o < n; o += (int64_t)buf.size()) {
+            const int64_t m = std::min<int64_t>((int64_t)buf.size(), n - o);
+            if (std::fread(buf.data(), sizeof(uint32_t), m, f) != (size_t)m) { std::fclose(f); return fail(AID_ERR_INVALID, "truncated index file"); }
+            HIP_TRY(hipMemcpy(cols[c]->p + o, buf.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+    e->n_tracks = 0;
+    e->h_tomb.clear();
+    if (int rc = ensure_tracks(e, nt, s)) { std::fclose(f); return rc; }
+    if (nt && std::fread(e->h_tomb.data(), 1, nt, f) != nt) { std::fclose(f); return fail(AID_ERR_INVALID, "truncated index file"); }
+    std::fclose(f);
+    if (nt) HIP_TRY(hipMemcpy(e->tomb.p, e->h_tomb.data(), nt, hipMemcpyHostToDevice));
+    e->n_post = n;
+    e->index_dirty = true;
+    e->index_built = false;
+    return AID_OK;
+}
+
+// run K5 over nq queries whose records are at device q_recs ranges (q_start/q_count device arrays)
+static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
+                       int nq, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
+    const int mr = e->cfg.max_results;
+    const int kBatch = 2048;
+    const size_t H = index_hist_words();
+    HIP_TRY(e->q_hist.reserve((size_t)std::min(nq, kBatch) * H));
+    if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5b re-zeroes its rows afterwards
+        HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
+        e->hist_zero_cap = e->q_hist.n;
+    }
+    HIP_TRY(e->q_rows.reserve((size_t)std::max(nq, 1) * mr * 5));
+    HIP_TRY(e->q_nrows.reserve((size_t)std::max(nq, 1)));
+    for (int q0 = 0; q0 < nq; q0 += kBatch) {
+        const int nb = std::min(kBatch, nq - q0);
+        {
+            ProfScope ps(e, AID_K_MATCH, s);
+            launch_query(recs, qstart_dev + q0, qcount_dev + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p,
+                         e->n_tracks, e->cfg.min_match, mr, e->q_hist.p, e->q_rows.p + (size_t)q0 * mr * 5,
+                         e->q_nrows.p + q0, s);
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(nrows, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    for (int q = 0; q < nq; ++q)
+        if (nrows[q] < 0) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
+    return AID_OK;
+}
+
+static int ensure_index(aid_engine *e) {
+    if (e->index_dirty || !e->index_built) return finalize_locked(e);
+    return AID_OK;
+}
+
+int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t nq, aid_match_row *rows,
+              int32_t *nrows) {
+    if (!e || nq < 0 || !qoff || (nq > 0 && (!rows || !nrows))) return fail(AID_ERR_INVALID, "aid_query: bad argument");
+    if (nq == 0) return AID_OK;
+    for (int q = 0; q < nq; ++q)
+        if (qoff[q + 1] < qoff[q]) return fail(AID_ERR_INVALID, "aid_query: offsets must be non-decreasing");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = ensure_index(e)) return rc;
+    hipStream_t s = e->own_stream;
+    const int64_t n = qoff[nq] - qoff[0];
+    HIP_TRY(e->q_recs.reserve((size_t)std::max<int64_t>(n, 1)));
+    HIP_TRY(e->q_start.reserve(nq));
+    HIP_TRY(e->q_count.reserve(nq));
+    std::vector<int64_t> st(nq), ct(nq);
+    for (int q = 0; q < nq; ++q) {
+        st[q] = qoff[q] - qoff[0];
+        ct[q] = qoff[q + 1] - qoff[q];
+    }
+    if (n > 0) HIP_TRY(hipMemcpyAsync(e->q_recs.p, recs + qoff[0], n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->q_start.p, st.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->q_count.p, ct.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, rows, nrows, s);
+}
+
+int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    if (!e->have_result) return fail(AID_ERR_STATE, "no extraction to query with");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = ensure_index(e)) return rc;
+    hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
+    const int nq = e->n_clips;
+    if (nq == 0) return AID_OK;
+    if (!rows || !nrows) return fail(AID_ERR_INVALID, "null output");
+    HIP_TRY(e->q_start.reserve(nq));
+    HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, rows, nrows, s);
 }
 
 }  // extern "C"

@@ -1,0 +1,309 @@
+// index.hip -- K4 index build and K5 match_vote (FPSPEC 7).
+//
+// Replaces the LMDB inverted index of the external `olaf_c` binary: `store`
+// (audio-ident-service/app/audio/fingerprint.py:117-125, single writer :7-8) and
+// `query` + offset voting (:185-202), whose per-track best bin becomes
+// OlafMatch.match_count (:44-50). SURVEY.md 8a rows a4, a5.
+//
+// Index (HBM): postings grouped by key26(hash) = k1 << 16 | k2 << 6 | dt (the 26
+// bits FPSPEC 6 can set), as a direct-address CSR:
+//   offsets u32[2^26 + 1]  (256 MB, one counting-sort pass, no comparison sort)
+//   post    u64[n]         (track | t_ref << 32)
+// Build = K4a count (one atomic per posting) -> exclusive scan -> K4b scatter.
+// Within a bucket the posting order is arrival order; FPSPEC 7 results are
+// order-independent sums/min/max, so queries are deterministic regardless.
+//
+// Query (one workgroup per query clip):
+//   K5a  every vote (track, d = t_ref - t_q) increments a hashed per-query
+//        histogram of 2^18 u32 (exact superset filter: a (track, d) with
+//        >= min_match votes has a bucket with >= min_match);
+//   K5b  re-enumerates only votes whose bucket passed into an exact LDS hash
+//        table {(track,d) -> count, tq_min, tq_max}, reduces best d per track
+//        (max count, then smallest d) with 64-bit LDS atomics, ranks the rows
+//        (count desc, track asc) and writes at most max_rows; it re-zeroes its
+//        histogram row for the next batch.
+#include "aidfp_device.h"
+
+namespace aid {
+
+constexpr int kKeyBits = 26;
+constexpr uint32_t kKeys = 1u << kKeyBits;
+constexpr int kHistBits = 18;
+constexpr uint32_t kHist = 1u << kHistBits;
+constexpr int kVoteCap = 4096;   // LDS (track, d) entries per query
+constexpr int kTrackCap = 1024;  // LDS per-track best entries per query
+
+__device__ __forceinline__ uint32_t key26(uint32_t h) {
+    return ((h >> 22) << 16) | (((h >> 12) & 0x3FFu) << 6) | (h & 0x3Fu);
+}
+
+__device__ __forceinline__ uint32_t mix_td(uint32_t track, int32_t d) {
+    uint32_t x = track * 0x9E3779B1u ^ ((uint32_t)d * 0x85EBCA77u);
+    x ^= x >> 15;
+    x *= 0x2C1B3C6Du;
+    x ^= x >> 12;
+    return x;
+}
+
+// ---- K4: build ----
+__global__ void k_index_count(const uint32_t *__restrict__ ph, const uint32_t *__restrict__ ptrack, int64_t n,
+                              const uint8_t *__restrict__ tomb, uint32_t n_tracks, uint32_t *__restrict__ cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t tr = ptrack[i];
+        if (tr < n_tracks && tomb[tr]) continue;
+        atomicAdd(&cnt[key26(ph[i])], 1u);
+    }
+}
+
+__global__ void k_index_scatter(const uint32_t *__restrict__ ph, const uint32_t *__restrict__ ptrack,
+                                const uint32_t *__restrict__ pt, int64_t n, const uint8_t *__restrict__ tomb,
+                                uint32_t n_tracks, uint32_t *__restrict__ cursor, uint64_t *__restrict__ post) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t tr = ptrack[i];
+        if (tr < n_tracks && tomb[tr]) continue;
+        const uint32_t pos = atomicAdd(&cursor[key26(ph[i])], 1u);
+        post[pos] = (uint64_t)tr | ((uint64_t)pt[i] << 32);
+    }
+}
+
+// exclusive scan of n u32 counts (n = k * 1024) -> out; block sums -> bsum
+__global__ __launch_bounds__(1024) void k_scan_blocks(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                     uint32_t *__restrict__ bsum, int64_t n) {
+    __shared__ uint32_t s[1024];
+    const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    const uint32_t v = i < n ? in[i] : 0u;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint32_t a = threadIdx.x >= off ? s[threadIdx.x - off] : 0u;
+        __syncthreads();
+        s[threadIdx.x] += a;
+        __syncthreads();
+    }
+    if (i < n) out[i] = s[threadIdx.x] - v;
+    if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
+}
+
+__global__ __launch_bounds__(1024) void k_scan_add(uint32_t *__restrict__ out, const uint32_t *__restrict__ boff,
+                                                  int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    if (i < n) out[i] += boff[blockIdx.x];
+}
+
+// extracted records of clip c -> postings (hash, track_ids[c], t) at dst_off[c]
+__global__ void k_records_to_postings(const uint64_t *__restrict__ recs, const int64_t *__restrict__ src_off,
+                                      const int64_t *__restrict__ counts, const int64_t *__restrict__ dst_off,
+                                      const uint32_t *__restrict__ track_ids, int n_clips, uint32_t *__restrict__ ph,
+                                      uint32_t *__restrict__ ptrack, uint32_t *__restrict__ pt) {
+    const int c = blockIdx.y;
+    if (c >= n_clips) return;
+    const int64_t n = counts[c];
+    const uint64_t *src = recs + src_off[c];
+    const int64_t o = dst_off[c];
+    const uint32_t tr = track_ids[c];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = src[i];
+        ph[o + i] = (uint32_t)r;
+        ptrack[o + i] = tr;
+        pt[o + i] = (uint32_t)(r >> 32);
+    }
+}
+
+void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
+                                const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
+                                uint32_t *ptrack, uint32_t *pt, hipStream_t s) {
+    if (n_clips <= 0) return;
+    hipLaunchKernelGGL(k_records_to_postings, dim3(16, n_clips), dim3(256), 0, s, recs, src_off, counts, dst_off,
+                       track_ids, n_clips, ph, ptrack, pt);
+}
+
+// ---- K5: query ----
+struct QueryParams {
+    const uint64_t *recs;      // query records (hash | tq << 32)
+    const int64_t *qstart;     // [nq] first record of query q (device)
+    const int64_t *qcount;     // [nq] records of query q (device)
+    int32_t nq;
+    const uint32_t *offsets;   // [2^26 + 1]
+    const uint64_t *post;
+    const uint8_t *tomb;
+    uint32_t n_tracks;
+    int32_t min_match;
+    int32_t max_rows;
+    uint32_t *hist;            // [nq][2^18], zero on entry, re-zeroed on exit
+    int32_t *rows;             // [nq][max_rows][5]
+    int32_t *nrows;            // [nq]; -1 = LDS table overflow (query not answered)
+};
+
+__global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
+    const int q = blockIdx.x;
+    const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
+    uint32_t *H = qp.hist + (int64_t)q * kHist;
+    for (int64_t i = a + threadIdx.x; i < z; i += blockDim.x) {
+        const uint64_t r = qp.recs[i];
+        const uint32_t k = key26((uint32_t)r);
+        const int32_t tq = (int32_t)(r >> 32);
+        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
+        for (uint32_t p = p0; p < p1; ++p) {
+            const uint64_t e = qp.post[p];
+            const uint32_t tr = (uint32_t)e;
+            if (qp.tomb[tr]) continue;
+            const int32_t d = (int32_t)(e >> 32) - tq;
+            atomicAdd(&H[mix_td(tr, d) & (kHist - 1)], 1u);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
+    __shared__ unsigned long long vkey[kVoteCap];  // (track << 32) | (uint32)d ; ~0 = empty
+    __shared__ uint32_t vcnt[kVoteCap], vmin[kVoteCap], vmax[kVoteCap];
+    __shared__ uint32_t tkey[kTrackCap];               // track ; ~0 = empty
+    __shared__ unsigned long long tbest[kTrackCap];    // count << 32 | ~(d + 2^31)
+    __shared__ int32_t out_n;
+    __shared__ int32_t overflow;
+    __shared__ int32_t rowbuf[kTrackCap][5];
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kVoteCap; i += blockDim.x) {
+        vkey[i] = ~0ull;
+        vcnt[i] = 0;
+        vmin[i] = 0xFFFFFFFFu;
+        vmax[i] = 0;
+    }
+    for (int i = tid; i < kTrackCap; i += blockDim.x) {
+        tkey[i] = 0xFFFFFFFFu;
+        tbest[i] = 0ull;
+    }
+    if (tid == 0) { out_n = 0; overflow = 0; }
+    __syncthreads();
+    const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
+    uint32_t *H = qp.hist + (int64_t)q * kHist;
+    const uint32_t mm = (uint32_t)qp.min_match;
+    // 1. exact table of candidate votes
+    for (int64_t i = a + tid; i < z; i += blockDim.x) {
+        const uint64_t r = qp.recs[i];
+        const uint32_t k = key26((uint32_t)r);
+        const int32_t tq = (int32_t)(r >> 32);
+        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
+        for (uint32_t p = p0; p < p1; ++p) {
+            const uint64_t e = qp.post[p];
+            const uint32_t tr = (uint32_t)e;
+            if (qp.tomb[tr]) continue;
+            const int32_t d = (int32_t)(e >> 32) - tq;
+            const uint32_t h = mix_td(tr, d);
+            if (H[h & (kHist - 1)] < mm) continue;
+            const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
+            uint32_t s = (h >> kHistBits) & (kVoteCap - 1);
+            int probes = 0;
+            for (;;) {
+                const unsigned long long old = atomicCAS(&vkey[s], ~0ull, key);
+                if (old == ~0ull || old == key) {
+                    atomicAdd(&vcnt[s], 1u);
+                    atomicMin(&vmin[s], (uint32_t)tq);
+                    atomicMax(&vmax[s], (uint32_t)tq);
+                    break;
+                }
+                if (++probes >= kVoteCap) { overflow = 1; break; }
+                s = (s + 1) & (kVoteCap - 1);
+            }
+        }
+    }
+    __syncthreads();
+    // 2. best d per track: max count, then smallest d
+    for (int s = tid; s < kVoteCap; s += blockDim.x) {
+        if (vkey[s] == ~0ull || vcnt[s] < mm) continue;
+        const uint32_t tr = (uint32_t)(vkey[s] >> 32);
+        const int32_t d = (int32_t)(uint32_t)vkey[s];
+        const unsigned long long packed = ((unsigned long long)vcnt[s] << 32) | (uint32_t)~((uint32_t)d + 0x80000000u);
+        uint32_t t = (tr * 0x9E3779B1u >> 22) & (kTrackCap - 1);
+        int probes = 0;
+        for (;;) {
+            const uint32_t old = atomicCAS(&tkey[t], 0xFFFFFFFFu, tr);
+            if (old == 0xFFFFFFFFu || old == tr) {
+                atomicMax(&tbest[t], packed);
+                break;
+            }
+            if (++probes >= kTrackCap) { overflow = 1; break; }
+            t = (t + 1) & (kTrackCap - 1);
+        }
+    }
+    __syncthreads();
+    // 3. emit one row per track from the winning (track, d) entry
+    for (int s = tid; s < kVoteCap; s += blockDim.x) {
+        if (vkey[s] == ~0ull || vcnt[s] < mm) continue;
+        const uint32_t tr = (uint32_t)(vkey[s] >> 32);
+        const int32_t d = (int32_t)(uint32_t)vkey[s];
+        const unsigned long long packed = ((unsigned long long)vcnt[s] << 32) | (uint32_t)~((uint32_t)d + 0x80000000u);
+        uint32_t t = (tr * 0x9E3779B1u >> 22) & (kTrackCap - 1);
+        for (int probes = 0; probes < kTrackCap && tkey[t] != tr; ++probes) t = (t + 1) & (kTrackCap - 1);
+        if (tkey[t] == tr && tbest[t] == packed) {
+            const int o = atomicAdd(&out_n, 1);
+            if (o < kTrackCap) {
+                rowbuf[o][0] = (int32_t)vcnt[s];
+                rowbuf[o][1] = (int32_t)tr;
+                rowbuf[o][2] = d;
+                rowbuf[o][3] = (int32_t)vmin[s];
+                rowbuf[o][4] = (int32_t)vmax[s];
+            }
+        }
+    }
+    __syncthreads();
+    // 4. rank (count desc, track asc) by counting rank, write the first max_rows
+    const int n = min(out_n, kTrackCap);
+    for (int i = tid; i < n; i += blockDim.x) {
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const bool before = rowbuf[j][0] > rowbuf[i][0] ||
+                                (rowbuf[j][0] == rowbuf[i][0] && (uint32_t)rowbuf[j][1] < (uint32_t)rowbuf[i][1]);
+            rank += before ? 1 : 0;
+        }
+        if (rank < qp.max_rows) {
+            int32_t *o = qp.rows + ((int64_t)q * qp.max_rows + rank) * 5;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) o[c] = rowbuf[i][c];
+        }
+    }
+    if (tid == 0) qp.nrows[q] = (overflow || out_n > kTrackCap) ? -1 : min(n, qp.max_rows);
+    // 5. re-zero this query's histogram row
+    for (int64_t i = tid; i < (int64_t)kHist; i += blockDim.x) H[i] = 0u;
+}
+
+void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
+                        uint32_t *cnt, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_index_count, dim3((unsigned)blocks), dim3(256), 0, s, ph, ptrack, n, tomb, n_tracks, cnt);
+}
+
+void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
+                          const uint8_t *tomb, uint32_t n_tracks, uint32_t *cursor, uint64_t *post, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_index_scatter, dim3((unsigned)blocks), dim3(256), 0, s, ph, ptrack, pt, n, tomb, n_tracks,
+                       cursor, post);
+}
+
+// exclusive scan of n counts (n multiple of 1024); tmp holds >= 2 * ceil(n/1024) + 1024 u32
+void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s) {
+    const int64_t nb = (n + 1023) / 1024;
+    uint32_t *bsum = tmp, *boff = tmp + nb, *b2 = tmp + 2 * nb;
+    hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(1024), 0, s, in, out, bsum, n);
+    if (nb > 1) {
+        // recursive on block sums (nb <= 2^16 for 2^26 keys -> at most two levels)
+        launch_scan(bsum, boff, nb, b2, s);
+        hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(1024), 0, s, out, boff, n);
+    }
+}
+
+void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
+                  const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
+                  uint32_t *hist, int32_t *rows, int32_t *nrows, hipStream_t s) {
+    if (nq <= 0) return;
+    QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, rows, nrows};
+    hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
+    hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(256), 0, s, qp);
+}
+
+uint32_t index_keys() { return kKeys; }
+uint32_t index_hist_words() { return kHist; }
+
+}  // namespace aid

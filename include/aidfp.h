@@ -42,7 +42,8 @@ extern "C" {
 #define AID_K_LANDMARK_COUNT 2
 #define AID_K_LANDMARK_WRITE 3
 #define AID_K_SYNTH 4
-#define AID_K_COUNT 5
+#define AID_K_MATCH 5
+#define AID_K_COUNT 6
 
 typedef struct aid_engine aid_engine;
 
@@ -113,6 +114,45 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
    [n_clips][n]: tracks/starts are HOST arrays; noise_a = query-noise half-width (0 = none). */
 int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips, int64_t n,
               int32_t noise_a, uint32_t salt, void *stream);
+
+/* ---- index + match (FPSPEC 7) ----
+ * Replaces `olaf_c store` + LMDB (fingerprint.py:117-125), `olaf_c del` (:239-246) and
+ * `olaf_c query` (:185-202). Postings accumulate on the device; the CSR is (re)built by
+ * aid_index_finalize, which aid_query* call implicitly when the index changed. Single
+ * writer: calls that mutate the index must be serialised by the caller (fingerprint.py:7-8). */
+
+/* one query result row (FPSPEC 7): d = t_ref - t_q of the best offset bin, in frames */
+typedef struct aid_match_row {
+    int32_t match_count;
+    uint32_t track;
+    int32_t d;
+    int32_t tq_min;
+    int32_t tq_max;
+} aid_match_row;
+
+int aid_index_reset(aid_engine *e);
+/* Add every clip of the last aid_extract as track track_ids[c] (host array of n_clips). */
+int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids);
+/* Add n postings (hash, track, t) from host (AID_PCM_HOST) or device (AID_PCM_DEVICE) arrays. */
+int aid_index_add_postings(aid_engine *e, const uint32_t *hash, const uint32_t *track, const uint32_t *t, int64_t n,
+                           int32_t location);
+/* Tombstone a track: its postings stop voting; AID_ERR_INVALID if unknown or already removed. */
+int aid_index_remove(aid_engine *e, uint32_t track);
+int aid_index_finalize(aid_engine *e);
+/* n_postings = stored postings, n_live = postings in the built CSR (-1 if stale), n_tracks = max id + 1 */
+int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks);
+/* Copy stored postings [first, first+count) to host or device columns (RCCL all-gather export). */
+int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t, int64_t first, int64_t count,
+                     int32_t location);
+/* Flat versioned file (magic AIDFPIX1 + header + posting columns + tombstones): replaces the OLAF_DB dir. */
+int aid_index_save(aid_engine *e, const char *path);
+int aid_index_load(aid_engine *e, const char *path);
+/* nq queries from host records: query q = recs[qoff[q] .. qoff[q+1]) (host qoff, nq+1 entries).
+   rows: host [nq][max_results]; nrows: host [nq]. */
+int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t nq, aid_match_row *rows,
+              int32_t *nrows);
+/* Query with every clip of the last aid_extract (records stay on the device). */
+int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows);
 
 /* Per-kernel timing with HIP events recorded on the launch stream. */
 int aid_profile_enable(aid_engine *e, int32_t on);

@@ -1,0 +1,39 @@
+"""The C-ABI library loads and exports every symbol include/aidfp.h declares (no GPU
+calls), and the ctypes signature table covers exactly that set."""
+
+import ctypes
+import re
+from pathlib import Path
+
+from aidfp import _lib
+
+HEADER = Path(__file__).resolve().parents[1] / "include" / "aidfp.h"
+
+
+def declared():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(aid_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    lib = ctypes.CDLL(str(_lib.LIB_PATH))
+    names = declared()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_signature_table_matches_header():
+    assert sorted(n for n, _, _ in _lib.SIGNATURES) == declared()
+
+
+def test_abi_version_and_defaults_without_gpu():
+    L = _lib.load()
+    assert L.aid_abi_version() == 1
+    cfg = _lib.AidConfig()
+    assert L.aid_config_default(44100, ctypes.byref(cfg)) == 0
+    assert (cfg.hop, cfg.min_match, cfg.max_results) == (512, 5, 50)
+    assert abs(cfg.peak_threshold - 4.0) < 1e-9
+    assert L.aid_config_default(16000, ctypes.byref(cfg)) == 0 and cfg.hop == 256
+    assert L.aid_config_default(0, ctypes.byref(cfg)) == _lib.AID_ERR_INVALID
+    assert "bad argument" in _lib.last_error()

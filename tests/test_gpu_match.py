@@ -1,0 +1,110 @@
+"""GPU parity for K4 index build + K5 match_vote vs the CPU oracle (oracle/fp_match.c,
+FPSPEC 7), plus the identification behaviour the reference's exact lane relies on
+(audio-ident-service/app/search/exact.py: best track first, offset recovered)."""
+
+import numpy as np
+import pytest
+
+import oracle as O
+from aidfp import synth
+from aidfp.engine import Engine
+
+pytestmark = pytest.mark.gpu
+SR = 44100
+HOP = 512
+N_TRACKS = 48
+TRACK_S = 30
+
+
+@pytest.fixture(scope="module")
+def catalog():
+    import torch
+
+    eng = Engine(SR)
+    n = SR * TRACK_S
+    pcm = torch.empty(N_TRACKS * n, dtype=torch.float32, device="cuda")
+    tracks = np.arange(N_TRACKS, dtype=np.uint32) + 500
+    eng.synth(pcm.data_ptr(), tracks, np.zeros(N_TRACKS, np.int64), n)
+    eng.extract_device(pcm.data_ptr(), np.arange(N_TRACKS + 1, dtype=np.int64) * n)
+    eng.index_add_extracted(tracks)
+    eng.index_finalize()
+    yield eng, tracks
+    eng.close()
+
+
+def _queries(tracks, rng, n_q=12, neg=3):
+    qs, truth = [], []
+    for i in range(n_q):
+        tr = int(tracks[rng.integers(len(tracks))])
+        start = int(rng.integers(0, (TRACK_S - 5) * SR))
+        qs.append(synth.synth(tr, start, 5 * SR, SR, snr_db=20.0, salt=100 + i))
+        truth.append((tr, start))
+    for i in range(neg):  # unseen tracks
+        qs.append(synth.synth(90000 + i, 0, 5 * SR, SR, snr_db=20.0, salt=7))
+        truth.append((None, 0))
+    return qs, truth
+
+
+def test_match_rows_equal_oracle(catalog):
+    eng, tracks = catalog
+    st = eng.index_stats()
+    post = eng.index_export()
+    assert st["postings"] == len(post) == st["live"] > 0
+    rng = np.random.default_rng(42)
+    qs, truth = _queries(tracks, rng)
+    # query records from the GPU extractor are bit-exact to the oracle's (tests/test_gpu_extract.py)
+    recs = [O.fingerprint(q, HOP) for q in qs]
+    got = eng.query(recs)
+    for q, (g, r) in enumerate(zip(got, recs)):
+        ref = O.query(post, r, min_match=eng.min_match, max_rows=eng.max_results)
+        assert np.array_equal(g, ref), f"query {q}: rows differ\n{g[:5]}\n{ref[:5]}"
+    # identification: true track ranked first, offset recovered to within one hop
+    for g, (tr, start) in zip(got, truth):
+        if tr is None:
+            assert len(g) == 0 or g[0, 0] < 20
+            continue
+        assert g[0, 1] == tr
+        assert abs(g[0, 2] * HOP - start) <= HOP
+
+
+def test_query_extracted_equals_host_query(catalog):
+    eng, tracks = catalog
+    rng = np.random.default_rng(7)
+    qs, _ = _queries(tracks, rng, n_q=6, neg=1)
+    recs = eng.extract_host(qs)
+    dev = eng.query_extracted()
+    host = eng.query(recs)
+    for a, b in zip(dev, host):
+        assert np.array_equal(a, b)
+
+
+def test_remove_and_save_load(catalog, tmp_path):
+    eng, tracks = catalog
+    rng = np.random.default_rng(3)
+    qs, truth = _queries(tracks, rng, n_q=4, neg=0)
+    recs = [O.fingerprint(q, HOP) for q in qs]
+    victim = truth[0][0]
+    path = tmp_path / "idx.aidfp"
+    eng.index_save(str(path))
+    eng.index_remove(victim)
+    with pytest.raises(Exception):
+        eng.index_remove(victim)  # already removed
+    post = eng.index_export()
+    live = post[post[:, 1] != victim]
+    got = eng.query(recs)
+    for g, r in zip(got, recs):
+        assert victim not in set(g[:, 1].tolist())
+        assert np.array_equal(g, O.query(live, r, min_match=eng.min_match, max_rows=eng.max_results))
+    # a fresh engine loading the saved file answers like the original did before the removal
+    with Engine(SR) as e2:
+        e2.index_load(str(path))
+        g2 = e2.query(recs)
+    for g, r in zip(g2, recs):
+        assert np.array_equal(g, O.query(post, r, min_match=eng.min_match, max_rows=eng.max_results))
+
+
+def test_empty_index_and_empty_query():
+    with Engine(16000) as eng:
+        eng.index_finalize()
+        out = eng.query([np.zeros(0, np.uint64), O.fingerprint(synth.synth(1, 0, 16000 * 4, 16000), 256)])
+        assert [len(o) for o in out] == [0, 0]
