@@ -1,0 +1,115 @@
+"""Catalog ingest sharded over the GPUs of one node (BASELINE config 3).
+
+The reference ingests one file at a time through a single LMDB writer
+(audio-ident-service/app/ingest/pipeline.py:294-310, fingerprint.py:7-8). Here
+every rank (one process per GPU) fingerprints its own shard of the tracks
+(extraction shards by track, no communication), then ONE exchange replicates
+the index: each rank's postings (hash, track, t) are all-gathered over RCCL /
+xGMI (torch.distributed "nccl" backend = RCCL on ROCm), so every GPU holds the
+whole catalog and can answer queries alone.
+
+RCCL has no all-gatherv: counts are all-gathered first, then every rank's
+postings padded to the largest count go through a single all_gather_into_tensor
+(one [world, max_n, 3] int32 buffer), and the padding is dropped on receive.
+`allgather_postings` is device-agnostic, so the same code runs under gloo on
+CPU tensors (tests/test_catalog_dist.py) and under RCCL on GPU tensors.
+"""
+
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def shard(tracks, rank: int, world: int):
+    """Contiguous block of the track list for `rank` (balanced to within one track)."""
+    n = len(tracks)
+    lo = (n * rank) // world
+    hi = (n * (rank + 1)) // world
+    return tracks[lo:hi]
+
+
+def allgather_postings(local, group=None):
+    """All-gather variable-length [n, 3] int32 posting blocks; returns [sum n, 3] in rank order."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    dev = local.device
+    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, n, group=group)
+    cnt = counts.cpu().tolist()
+    mx = max(cnt)
+    if mx == 0:
+        return local.new_zeros((0, 3))
+    send = local.new_zeros((mx, 3))
+    send[: local.shape[0]] = local
+    recv = local.new_empty((world * mx, 3))
+    dist.all_gather_into_tensor(recv, send, group=group)
+    recv = recv.view(world, mx, 3)
+    return torch.cat([recv[r, : cnt[r]] for r in range(world)], dim=0)
+
+
+@dataclass
+class IngestStats:
+    tracks_local: int
+    audio_s_local: float
+    postings_local: int
+    postings_total: int
+    t_extract: float
+    t_exchange: float
+    t_build: float
+
+
+def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=None) -> IngestStats:
+    """Fingerprint this rank's shard of synthetic tracks on its GPU, replicate the index.
+
+    `track_ids` is the full catalog (global ids); with torch.distributed initialised
+    each rank takes shard(track_ids, rank, world), otherwise the whole list."""
+    import torch
+    import torch.distributed as dist
+
+    distributed = dist.is_available() and dist.is_initialized()
+    rank = dist.get_rank(group) if distributed else 0
+    world = dist.get_world_size(group) if distributed else 1
+    mine = np.asarray(shard(np.asarray(track_ids, dtype=np.uint32), rank, world), dtype=np.uint32)
+    n = int(round(seconds * eng.sample_rate)) & ~1
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pcm = torch.empty(max(1, min(batch, len(mine))) * n, dtype=torch.float32, device="cuda")
+    base = eng.index_stats()["postings"]
+    for b0 in range(0, len(mine), batch):
+        tr = mine[b0 : b0 + batch]
+        eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n)
+        eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n)
+        eng.index_add_extracted(tr)
+    del pcm
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    n_local = eng.index_stats()["postings"] - base
+    total = n_local
+    if world > 1:
+        cols = torch.empty((3, max(n_local, 1)), dtype=torch.int32, device="cuda")
+        eng.index_export_device(cols[0].data_ptr(), cols[1].data_ptr(), cols[2].data_ptr(), base, n_local)
+        local = cols[:, :n_local].t().contiguous()
+        allp = allgather_postings(local, group)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        # replace this rank's postings by the gathered catalog (own shard included, rank order)
+        keep = eng.index_export(0, base) if base else None
+        eng.index_reset()
+        if keep is not None and len(keep):
+            k = torch.from_numpy(keep.astype(np.int32)).cuda().t().contiguous()
+            eng.index_add_postings(k[0].data_ptr(), k[1].data_ptr(), k[2].data_ptr(), k.shape[1])
+        g = allp.t().contiguous()
+        eng.index_add_postings(g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(), g.shape[1])
+        total = int(g.shape[1])
+    else:
+        t2 = t1
+    eng.index_finalize()
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    return IngestStats(len(mine), len(mine) * n / eng.sample_rate, n_local, total, t1 - t0, t2 - t1, t3 - t2)

@@ -37,9 +37,9 @@ void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, co
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
-                  uint32_t *hist, int32_t *rows, int32_t *nrows, hipStream_t s);
+                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s);
+void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 uint32_t index_keys();
-uint32_t index_hist_words();
 }  // namespace aid
 
 using namespace aid;
@@ -116,6 +116,8 @@ struct aid_engine {
     DevBuf<uint64_t> idx_post;
     bool index_built = false, index_dirty = true;
     int64_t n_indexed = 0;
+    int64_t n_buckets_used = 0;
+    DevBuf<unsigned long long> nz;
     // query workspaces
     DevBuf<uint64_t> q_recs;
     DevBuf<int64_t> q_start, q_count;
@@ -201,7 +203,7 @@ int aid_config_default(int32_t sample_rate, aid_config *out) {
     out->hop = sample_rate >= 32000 ? 512 : 256;
     out->peak_threshold = 4.0f;
     out->device = -1;
-    out->min_match = 5;
+    out->min_match = 8;
     out->max_results = 50;
     return AID_OK;
 }
@@ -216,7 +218,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
         return fail(AID_ERR_INVALID, "hop must be one of 128, 256, 512, 1024, 2048");
     if (c.peak_threshold == 0.0f) c.peak_threshold = 4.0f;
     if (!(c.peak_threshold > 0.0f)) return fail(AID_ERR_INVALID, "peak_threshold must be > 0");
-    if (c.min_match <= 0) c.min_match = 5;
+    if (c.min_match <= 0) c.min_match = 8;
     if (c.max_results <= 0) c.max_results = 50;
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -283,6 +285,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->idx_off.release();
     e->scan_tmp.release();
     e->idx_post.release();
+    e->nz.release();
     e->q_recs.release();
     e->q_start.release();
     e->q_count.release();
@@ -705,6 +708,9 @@ static int finalize_locked(aid_engine *e) {
     if (e->n_tracks == 0) HIP_TRY(e->tomb.reserve(1024));
     HIP_TRY(hipMemsetAsync(e->idx_cnt.p, 0, K * sizeof(uint32_t), s));
     launch_index_count(e->p_hash.p, e->p_track.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p, s);
+    HIP_TRY(e->nz.reserve(1));
+    HIP_TRY(hipMemsetAsync(e->nz.p, 0, sizeof(unsigned long long), s));
+    launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
     launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
     HIP_TRY(hipMemcpyAsync(e->idx_cnt.p, e->idx_off.p, K * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     launch_index_scatter(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p,
@@ -712,7 +718,10 @@ static int finalize_locked(aid_engine *e) {
     HIP_TRY(hipGetLastError());
     uint32_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, e->idx_off.p + (K - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    unsigned long long used = 0;
+    HIP_TRY(hipMemcpyAsync(&used, e->nz.p, sizeof(used), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    e->n_buckets_used = (int64_t)used;
     e->n_indexed = total;
     e->index_built = true;
     e->index_dirty = false;
@@ -812,34 +821,78 @@ int aid_index_load(aid_engine *e, const char *path) {
     return AID_OK;
 }
 
-// run K5 over nq queries whose records are at device q_recs ranges (q_start/q_count device arrays)
+// run K5 over nq queries whose records are at device ranges (q_start/q_count device arrays).
+// max_recs = the largest query (host-known); the vote histogram gets ~8 buckets per
+// expected vote; queries whose exact LDS table overflowed are re-run with 4x the buckets.
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
-                       int nq, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
+                       int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
     const int mr = e->cfg.max_results;
-    const int kBatch = 2048;
-    const size_t H = index_hist_words();
-    HIP_TRY(e->q_hist.reserve((size_t)std::min(nq, kBatch) * H));
-    if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5b re-zeroes its rows afterwards
-        HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
-        e->hist_zero_cap = e->q_hist.n;
-    }
     HIP_TRY(e->q_rows.reserve((size_t)std::max(nq, 1) * mr * 5));
     HIP_TRY(e->q_nrows.reserve((size_t)std::max(nq, 1)));
-    for (int q0 = 0; q0 < nq; q0 += kBatch) {
-        const int nb = std::min(kBatch, nq - q0);
-        {
-            ProfScope ps(e, AID_K_MATCH, s);
-            launch_query(recs, qstart_dev + q0, qcount_dev + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p,
-                         e->n_tracks, e->cfg.min_match, mr, e->q_hist.p, e->q_rows.p + (size_t)q0 * mr * 5,
-                         e->q_nrows.p + q0, s);
-        }
-        HIP_TRY(hipGetLastError());
-    }
-    HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(nrows, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    std::vector<int> todo(nq);
+    for (int q = 0; q < nq; ++q) todo[q] = q;
+    std::vector<int64_t> h_start(nq), h_count(nq);
+    HIP_TRY(hipMemcpyAsync(h_start.data(), qstart_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_count.data(), qcount_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    for (int q = 0; q < nq; ++q)
-        if (nrows[q] < 0) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
+    if (max_recs < 0)
+        for (int q = 0; q < nq; ++q) max_recs = std::max(max_recs, h_count[q]);
+    const double per_bucket = e->n_buckets_used > 0 ? (double)e->n_indexed / (double)e->n_buckets_used : 1.0;
+    const double votes = std::max(1.0, (double)max_recs * per_bucket);
+    int bits = 16;
+    while (bits < 24 && (double)(1ull << bits) < 8.0 * votes) ++bits;
+    for (int attempt = 0; !todo.empty(); ++attempt, bits += 2) {
+        if (bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
+        const size_t H = (size_t)1 << bits;
+        const int batch = (int)std::max<size_t>(1, std::min<size_t>(2048, ((size_t)4 << 30) / (H * 4)));
+        HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
+        if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5b re-zeroes its rows afterwards
+            HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
+            e->hist_zero_cap = e->q_hist.n;
+        }
+        const int64_t *qs = qstart_dev, *qc = qcount_dev;
+        int32_t *out_rows = e->q_rows.p, *out_n = e->q_nrows.p;
+        std::vector<int> order = todo;
+        if (attempt > 0) {  // gather the overflowed queries' ranges into the scratch arrays' tail
+            HIP_TRY(e->x_src.reserve(2 * order.size()));
+            std::vector<int64_t> st(order.size()), ct(order.size());
+            for (size_t i = 0; i < order.size(); ++i) { st[i] = h_start[order[i]]; ct[i] = h_count[order[i]]; }
+            HIP_TRY(hipMemcpyAsync(e->x_src.p, st.data(), st.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(e->x_src.p + order.size(), ct.data(), ct.size() * sizeof(int64_t),
+                                   hipMemcpyHostToDevice, s));
+            qs = e->x_src.p;
+            qc = e->x_src.p + order.size();
+            HIP_TRY(e->x_dst.reserve(((size_t)order.size() * mr * 5 + 1) / 2 + order.size()));
+            out_rows = reinterpret_cast<int32_t *>(e->x_dst.p);
+            out_n = out_rows + (size_t)order.size() * mr * 5;
+        }
+        const int n = (int)order.size();
+        for (int q0 = 0; q0 < n; q0 += batch) {
+            const int nb = std::min(batch, n - q0);
+            {
+                ProfScope ps(e, AID_K_MATCH, s);
+                launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
+                             e->cfg.min_match, mr, e->q_hist.p, bits, out_rows + (size_t)q0 * mr * 5, out_n + q0, s);
+            }
+            HIP_TRY(hipGetLastError());
+        }
+        std::vector<int32_t> got_n(n);
+        std::vector<aid_match_row> got((size_t)n * mr);
+        HIP_TRY(hipMemcpyAsync(got.data(), out_rows, (size_t)n * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(got_n.data(), out_n, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int> again;
+        for (int i = 0; i < n; ++i) {
+            const int q = order[i];
+            if (got_n[i] < 0) {
+                again.push_back(q);
+                continue;
+            }
+            nrows[q] = got_n[i];
+            std::memcpy(rows + (size_t)q * mr, got.data() + (size_t)i * mr, (size_t)mr * sizeof(aid_match_row));
+        }
+        todo.swap(again);
+    }
     return AID_OK;
 }
 
@@ -869,7 +922,9 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
     if (n > 0) HIP_TRY(hipMemcpyAsync(e->q_recs.p, recs + qoff[0], n * sizeof(uint64_t), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(e->q_start.p, st.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(e->q_count.p, ct.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, rows, nrows, s);
+    int64_t mx = 0;
+    for (int q = 0; q < nq; ++q) mx = std::max(mx, ct[q]);
+    return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, mx, rows, nrows, s);
 }
 
 int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
@@ -883,7 +938,7 @@ int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
     if (!rows || !nrows) return fail(AID_ERR_INVALID, "null output");
     HIP_TRY(e->q_start.reserve(nq));
     HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, rows, nrows, s);
+    return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, -1, rows, nrows, s);
 }
 
 }  // extern "C"

@@ -15,8 +15,9 @@
 //
 // Query (one workgroup per query clip):
 //   K5a  every vote (track, d = t_ref - t_q) increments a hashed per-query
-//        histogram of 2^18 u32 (exact superset filter: a (track, d) with
-//        >= min_match votes has a bucket with >= min_match);
+//        histogram of 2^b u32 (exact superset filter: a (track, d) with
+//        >= min_match votes has a bucket with >= min_match); b is sized by the
+//        host from the index's mean bucket length and widened on overflow;
 //   K5b  re-enumerates only votes whose bucket passed into an exact LDS hash
 //        table {(track,d) -> count, tq_min, tq_max}, reduces best d per track
 //        (max count, then smallest d) with 64-bit LDS atomics, ranks the rows
@@ -28,8 +29,6 @@ namespace aid {
 
 constexpr int kKeyBits = 26;
 constexpr uint32_t kKeys = 1u << kKeyBits;
-constexpr int kHistBits = 18;
-constexpr uint32_t kHist = 1u << kHistBits;
 constexpr int kVoteCap = 4096;   // LDS (track, d) entries per query
 constexpr int kTrackCap = 1024;  // LDS per-track best entries per query
 
@@ -129,7 +128,8 @@ struct QueryParams {
     uint32_t n_tracks;
     int32_t min_match;
     int32_t max_rows;
-    uint32_t *hist;            // [nq][2^18], zero on entry, re-zeroed on exit
+    uint32_t *hist;            // [nq][2^hist_bits], zero on entry, re-zeroed on exit
+    int32_t hist_bits;
     int32_t *rows;             // [nq][max_rows][5]
     int32_t *nrows;            // [nq]; -1 = LDS table overflow (query not answered)
 };
@@ -137,7 +137,8 @@ struct QueryParams {
 __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
     const int q = blockIdx.x;
     const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
-    uint32_t *H = qp.hist + (int64_t)q * kHist;
+    const uint32_t hmask = (1u << qp.hist_bits) - 1;
+    uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
     for (int64_t i = a + threadIdx.x; i < z; i += blockDim.x) {
         const uint64_t r = qp.recs[i];
         const uint32_t k = key26((uint32_t)r);
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
             const uint32_t tr = (uint32_t)e;
             if (qp.tomb[tr]) continue;
             const int32_t d = (int32_t)(e >> 32) - tq;
-            atomicAdd(&H[mix_td(tr, d) & (kHist - 1)], 1u);
+            atomicAdd(&H[mix_td(tr, d) & hmask], 1u);
         }
     }
 }
@@ -176,7 +177,8 @@ __global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
     if (tid == 0) { out_n = 0; overflow = 0; }
     __syncthreads();
     const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
-    uint32_t *H = qp.hist + (int64_t)q * kHist;
+    const uint32_t hmask = (1u << qp.hist_bits) - 1;
+    uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
     const uint32_t mm = (uint32_t)qp.min_match;
     // 1. exact table of candidate votes
     for (int64_t i = a + tid; i < z; i += blockDim.x) {
@@ -190,9 +192,9 @@ __global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
             if (qp.tomb[tr]) continue;
             const int32_t d = (int32_t)(e >> 32) - tq;
             const uint32_t h = mix_td(tr, d);
-            if (H[h & (kHist - 1)] < mm) continue;
+            if (H[h & hmask] < mm) continue;
             const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
-            uint32_t s = (h >> kHistBits) & (kVoteCap - 1);
+            uint32_t s = (h >> 20) & (kVoteCap - 1);
             int probes = 0;
             for (;;) {
                 const unsigned long long old = atomicCAS(&vkey[s], ~0ull, key);
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
     }
     if (tid == 0) qp.nrows[q] = (overflow || out_n > kTrackCap) ? -1 : min(n, qp.max_rows);
     // 5. re-zero this query's histogram row
-    for (int64_t i = tid; i < (int64_t)kHist; i += blockDim.x) H[i] = 0u;
+    for (int64_t i = tid; i <= (int64_t)hmask; i += blockDim.x) H[i] = 0u;
 }
 
 void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
@@ -296,14 +298,27 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
-                  uint32_t *hist, int32_t *rows, int32_t *nrows, hipStream_t s) {
+                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s) {
     if (nq <= 0) return;
-    QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, rows, nrows};
+    QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
+                   nrows};
     hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(256), 0, s, qp);
 }
 
+// number of non-empty buckets (for the query histogram sizing)
+__global__ void k_count_nonzero(const uint32_t *__restrict__ cnt, int64_t n, unsigned long long *__restrict__ out) {
+    unsigned long long c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        c += cnt[i] != 0u;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, c);
+}
+
+void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_count_nonzero, dim3(2048), dim3(256), 0, s, cnt, n, out);
+}
+
 uint32_t index_keys() { return kKeys; }
-uint32_t index_hist_words() { return kHist; }
 
 }  // namespace aid

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""BASELINE config 4: noisy 5 s query clips matched against a GPU-resident index, 1 GPU.
+
+    python bench_match.py --tracks 100000 --queries 10000
+
+Index: `--tracks` synthetic tracks x 30 s (aid_synth in HBM, K1-K4). Queries:
+5 s clips at offsets uniform in [0, 25] s (scripts/build_eval_corpus.py:481-483)
+with white noise at SNR 20 dB (:154-198, :602-606), plus `--neg-frac` clips of
+unseen tracks. Every <= 5 s clip is queried as the reference's three sub-windows
+(app/search/exact.py:48-52, :103) -- 3 engine queries per clip -- and merged
+with the exact lane's consensus (aidfp.exact). The timed region is the GPU work:
+sub-window extraction (K1-K3) + match (K5) for all clips, inputs in HBM.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+import uuid
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent / "audio-ident_amd"))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tracks", type=int, default=100000)
+    ap.add_argument("--seconds", type=float, default=30.0)
+    ap.add_argument("--queries", type=int, default=10000)
+    ap.add_argument("--neg-frac", type=float, default=0.1)
+    ap.add_argument("--snr", type=float, default=20.0)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--sr", type=int, default=44100)
+    ap.add_argument("--min-match", type=int, default=0, help="engine min_match (0 = FPSPEC default)")
+    args = ap.parse_args()
+
+    import torch
+
+    from aidfp import exact as ex
+    from aidfp import synth
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.engine import Engine
+    from aidfp.fingerprint import OlafMatch
+
+    torch.cuda.set_device(0)
+    eng = Engine(args.sr, device=0, min_match=args.min_match)
+    t0 = time.perf_counter()
+    st = ingest_synthetic(eng, np.arange(args.tracks, dtype=np.uint32), args.seconds)
+    t_index = time.perf_counter() - t0
+
+    rng = np.random.default_rng(42)
+    n_pos = args.queries
+    n_neg = int(round(args.queries * args.neg_frac))
+    truth = np.concatenate([rng.integers(0, args.tracks, n_pos), np.arange(n_neg) + args.tracks + 10**6]).astype(np.uint32)
+    starts = np.concatenate([rng.integers(0, int(25 * args.sr), n_pos), np.zeros(n_neg, np.int64)]).astype(np.int64)
+    nq = len(truth)
+    wins = [(0.0, 3.5), (0.75, 4.25), (1.5, 5.0)]
+    wlen = int(3.5 * args.sr) & ~1
+    noise_a = synth.noise_halfwidth(args.snr)
+    sec = eng.hop / eng.sample_rate
+    all_rows = [None] * (3 * nq)
+    pcm = torch.empty(min(3 * nq, 3 * args.batch) * wlen, dtype=torch.float32, device="cuda")
+    t_gpu = 0.0
+    for q0 in range(0, nq, args.batch):
+        qs = np.arange(q0, min(nq, q0 + args.batch))
+        tr = np.repeat(truth[qs], 3)
+        stt = (np.repeat(starts[qs], 3) + np.tile([int(a * args.sr) for a, _ in wins], len(qs))).astype(np.int64)
+        eng.synth(pcm.data_ptr(), tr, stt, wlen, noise_a=noise_a, salt=77)
+        offs = np.arange(len(tr) + 1, dtype=np.int64) * wlen
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        eng.extract_device(pcm.data_ptr(), offs)
+        rows = eng.query_extracted()
+        torch.cuda.synchronize()
+        t_gpu += time.perf_counter() - t1
+        for i, r in enumerate(rows):
+            all_rows[3 * q0 + i] = r
+
+    t2 = time.perf_counter()
+    top1 = 0
+    fp_hits = 0
+    off_err = []
+    neg_best = []
+    for q in range(nq):
+        windows = []
+        for w in range(3):
+            ms = []
+            for cnt, track, d, tq0, tq1 in all_rows[3 * q + w].tolist():
+                ms.append(OlafMatch(cnt, tq0 * sec, tq1 * sec, str(uuid.UUID(int=int(track) + 1)), int(track),
+                                    (tq0 + d) * sec, (tq1 + d) * sec))
+            windows.append(ms)
+        ranked = ex.rank(ex.consensus_score(windows), 10)
+        if q < n_pos:
+            if ranked and ranked[0].track_uuid.int - 1 == int(truth[q]):
+                top1 += 1
+                off_err.append(abs(ranked[0].offset_seconds - (starts[q] / args.sr + 0.75)))
+        else:
+            neg_best.append(max((sum(int(r[0]) for r in all_rows[3 * q + w][:1]) for w in range(3)), default=0))
+            if ranked:
+                fp_hits += 1
+    t_host = time.perf_counter() - t2
+
+    print(json.dumps({
+        "metric": "exact-lane queries/sec (5 s clips, 3 sub-window queries each), 1 GPU",
+        "value": round(nq / t_gpu, 1), "unit": "clips/s", "engine_queries_per_s": round(3 * nq / t_gpu, 1),
+        "audio_s_per_s": round(3 * nq * 3.5 / t_gpu, 1), "n_gpus": 1,
+        "clips": nq, "positives": n_pos, "negatives": n_neg, "snr_db": args.snr,
+        "top1_accuracy": round(top1 / max(1, n_pos), 4), "false_positive_rate": round(fp_hits / max(1, n_neg), 4),
+        "median_offset_error_s": round(float(np.median(off_err)), 4) if off_err else None,
+        "engine_min_match": eng.min_match,
+        "neg_best_window_count_pcts": [int(np.percentile(neg_best, p)) for p in (50, 90, 99)] if neg_best else None,
+        "gpu_s": round(t_gpu, 3), "host_consensus_s": round(t_host, 3), "index_build_s": round(t_index, 3),
+        "index_tracks": args.tracks, "index_postings": st.postings_total, "data": "synthetic",
+    }), flush=True)
+    eng.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
