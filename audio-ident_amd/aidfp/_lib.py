@@ -93,6 +93,7 @@ SIGNATURES = [
     ("aid_index_load", ctypes.c_int, [P, ctypes.c_char_p]),
     ("aid_query", ctypes.c_int, [P, P, P, I32, P, P]),
     ("aid_query_extracted", ctypes.c_int, [P, P, P]),
+    ("aid_downmix", ctypes.c_int, [P, P, I64, P, P]),
     ("aid_profile_enable", ctypes.c_int, [P, I32]),
     ("aid_profile_read", ctypes.c_int, [P, P, P, I32]),
 ]

@@ -239,6 +239,10 @@ class Engine:
         check(self._lib.aid_query_extracted(self._h, ctypes.addressof(rows), _p(nrows)))
         return self._rows(rows, nrows, nq)
 
+    def downmix(self, stereo_ptr: int, n_frames: int, mono_ptr: int, stream: int | None = None) -> None:
+        check(self._lib.aid_downmix(self._h, ctypes.c_void_p(stereo_ptr), int(n_frames), ctypes.c_void_p(mono_ptr),
+                                    ctypes.c_void_p(stream) if stream else None))
+
     # -- profiling --
     def profile_enable(self, on: bool = True) -> None:
         check(self._lib.aid_profile_enable(self._h, 1 if on else 0))

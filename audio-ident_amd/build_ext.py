@@ -20,7 +20,7 @@ LIB = PKG / "aidfp" / "libaidfp.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "engine.cpp"]
+SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "stream.hip", "engine.cpp"]
 FLAGS = [
     f"--offload-arch={ARCH}",
     "-O3",

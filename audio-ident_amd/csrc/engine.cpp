@@ -40,6 +40,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
                   uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 uint32_t index_keys();
+void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
 }  // namespace aid
 
 using namespace aid;
@@ -942,3 +943,13 @@ int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
 }
 
 }  // extern "C"
+
+extern "C" int aid_downmix(aid_engine *e, const float *stereo, int64_t n_frames, float *mono, void *stream) {
+    if (!e || n_frames < 0 || (n_frames > 0 && (!stereo || !mono))) return fail(AID_ERR_INVALID, "aid_downmix: bad argument");
+    if (((uintptr_t)stereo & 15) || ((uintptr_t)mono & 7)) return fail(AID_ERR_INVALID, "aid_downmix: misaligned buffers");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = pick_stream(e, stream);
+    launch_downmix(stereo, n_frames, mono, s);
+    HIP_TRY(hipGetLastError());
+    return AID_OK;
+}

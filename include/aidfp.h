@@ -154,6 +154,11 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
 /* Query with every clip of the last aid_extract (records stay on the device). */
 int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows);
 
+/* Streaming front end (config 5): interleaved f32 stereo [n_frames][2] -> mono [n_frames] on the
+   device, m = (L + R) * 0.5f (the ffmpeg -ac 1 role, decode.py:50-51). Device pointers, stereo
+   16-byte and mono 8-byte aligned; asynchronous on `stream`. */
+int aid_downmix(aid_engine *e, const float *stereo, int64_t n_frames, float *mono, void *stream);
+
 /* Per-kernel timing with HIP events recorded on the launch stream. */
 int aid_profile_enable(aid_engine *e, int32_t on);
 /* ms[AID_K_COUNT] summed device time, launches[AID_K_COUNT]; synchronises; reset != 0 clears. */
