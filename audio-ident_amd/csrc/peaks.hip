@@ -11,9 +11,10 @@
 //   * rows are staged in LDS 4 at a time (double-buffered, one barrier per 4
 //     rows); each thread reads its +-15-bin neighbours from LDS;
 //   * the vertical +-7-frame part is register-resident: `before` is complete when a
-//     row arrives (the previous 7 rows' row-max live in an 8-slot register ring),
-//     `after` is an accumulator that the next 7 rows max into; ring slots are
-//     compile-time because the row loop is unrolled by 8;
+//     row arrives (the previous 7 rows' row-max live in an 8-slot register ring); a
+//     candidate then stays pending until each of the next 7 rows' row-max has been
+//     checked against it (<= keeps it, > knocks it out); ring slots are compile-time
+//     because the row loop is unrolled by 8;
 //   * a decided row is emitted with 4 wave ballots (one per bin offset i < 4): mask
 //     word 4*w + i of a frame holds, at bit l, the peak flag of bin 256*w + 4*l + i
 //     ("ballot layout"; K3 and aidfp.engine.peaks_from_mask unshuffle it).
@@ -64,12 +65,11 @@ __global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ pow
     }
 
     float fh[8][4];    // row-max (Full) of recent rows, slot = iteration & 7
-    float pend[8][4];  // candidate power of pending rows (-1 = not a candidate)
-    float acc[8][4];   // running `after` max of pending rows
+    float pend[8][4];  // power of pending candidates not yet beaten by a later row (-1 = none)
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { fh[s][i] = 0.f; pend[s][i] = -1.f; acc[s][i] = 0.f; }
+        for (int i = 0; i < 4; ++i) { fh[s][i] = 0.f; pend[s][i] = -1.f; }
     const float kmin_ok = (tid == 0) ? 0.f : 1.f;  // bin 0 is never a peak
 
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
@@ -138,14 +138,18 @@ __global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ pow
 #pragma unroll
                 for (int d = 1; d <= 7; ++d) bf = fmaxf(bf, fh[(s - d) & 7][i]);
                 const float okf = (i == 0 ? kmin_ok : 1.f) * row_ok;
-                const bool cand = (p > bf) & (okf > 0.f);
+                // `after` part of this row: the right window (p >= R); later rows test below
+                const bool cand = (p > bf) & (p >= R[i]) & (okf > 0.f);
+                // this row's Full knocks out pending candidates of rows r-1 .. r-7 it exceeds
 #pragma unroll
-                for (int d = 1; d <= 7; ++d) acc[(s - d) & 7][i] = fmaxf(acc[(s - d) & 7][i], fm);
-                // row r-7 (slot s-7 == s+1) now has its complete `after`
-                pk[i] = pend[(s + 1) & 7][i] >= acc[(s + 1) & 7][i];
+                for (int d = 1; d <= 7; ++d) {
+                    float &pe = pend[(s - d) & 7][i];
+                    pe = (fm <= pe) ? pe : -1.f;
+                }
+                // row r-7 (slot s-7 == s+1) has now met all 7 later rows
+                pk[i] = pend[(s + 1) & 7][i] >= 0.f;
                 fh[s][i] = fm;
                 pend[s][i] = cand ? p : -1.f;
-                acc[s][i] = R[i];
             }
             const uint64_t b0 = __ballot(pk[0]), b1 = __ballot(pk[1]), b2 = __ballot(pk[2]), b3 = __ballot(pk[3]);
             const int64_t rd = r - kPeakDT;

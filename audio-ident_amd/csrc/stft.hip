@@ -18,8 +18,9 @@
 //   * stage B = 16-point DFT in registers, twiddle, quad exchange through LDS
 //     (E2, lane stride 17 float2);
 //   * stage C = radix-4 in registers, spill to LDS in XOR-swizzled natural order
-//     (E3), then the real split reads Z[k] and Z[1024-k] (both conflict-free) and
-//     stores 64 consecutive bins per wave-instruction.
+//     (E3), then the real split reads each mirror pair (Z[k], Z[1024-k]) once
+//     (conflict-free) and produces both bins; stores are 64 consecutive bins per
+//     wave-instruction (the mirror bins in descending order, same 256-B segment).
 // A workgroup is 12 waves (3 per SIMD) sharing 32 KB of tables in LDS; the
 // exchanges are wave-private, so there is no workgroup barrier in the loop.
 #include "aidfp_device.h"
@@ -138,19 +139,40 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 }
                 wave_lds_sync();
                 float *drow = dst + (int64_t)f * kBins;
+                // real split, bins in mirror pairs (k, 1024-k): one read of Z[k], Z[1024-k] serves
+                // both. For bin 1024-k the FPSPEC sums are the same exact values with signs
+                // flipped (a+c, c+a commute; b-d = -(d-b)), so both bins stay bit-exact.
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int k = lane + 64 * i;
-                    const int kk = AID_K1_DIAG == 2 ? (k ^ 512) : (1024 - k) & 1023;
+                for (int i = 0; i < 8; ++i) {
+                    const int k = lane + 64 * i;  // 0..511
+                    const int kk = (1024 - k) & 1023;
                     const float2 a = buf[e3(k)];
-                    const float2 b = buf[e3(kk)];
-                    const float2 o = make_float2(a.y + b.y, b.x - a.x);
+                    const float2 b = buf[e3(AID_K1_DIAG == 2 ? (k ^ 512) : kk)];
                     const float er = a.x + b.x, ei = a.y - b.y;
-                    const float2 tw = cmul(o, s_t2k[k]);
+                    const float orr = a.y + b.y, oi = b.x - a.x;
+                    {
+                        const float2 tw = cmul(make_float2(orr, oi), s_t2k[k]);
+                        const float xr = er + tw.x, xi = ei + tw.y;
+                        const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                        if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
+                        else drow[k] = P;
+                    }
+                    if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
+                        const float2 tw = cmul(make_float2(orr, -oi), s_t2k[1024 - k]);
+                        const float xr = er + tw.x, xi = -ei + tw.y;
+                        const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                        if constexpr (LOGMAG) drow[1024 - k] = 10.0f * log10f(P + 1e-10f);
+                        else drow[1024 - k] = P;
+                    }
+                }
+                if (lane == 0) {  // bin 512 pairs with itself
+                    const float2 a = buf[e3(512)];
+                    const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
+                    const float2 tw = cmul(make_float2(orr, oi), s_t2k[512]);
                     const float xr = er + tw.x, xi = ei + tw.y;
                     const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
-                    if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
-                    else drow[k] = P;
+                    if constexpr (LOGMAG) drow[512] = 10.0f * log10f(P + 1e-10f);
+                    else drow[512] = P;
                 }
                 wave_lds_sync();
             }
