@@ -39,6 +39,9 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
+void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
+                      const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
+                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, hipStream_t s);
 uint32_t index_keys();
 void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
 }  // namespace aid
@@ -118,6 +121,7 @@ struct aid_engine {
     bool index_built = false, index_dirty = true;
     int64_t n_indexed = 0;
     int64_t n_buckets_used = 0;
+    int64_t n_fallback = 0;  // queries answered by the global-histogram path
     DevBuf<unsigned long long> nz;
     // query workspaces
     DevBuf<uint64_t> q_recs;
@@ -204,7 +208,7 @@ int aid_config_default(int32_t sample_rate, aid_config *out) {
     out->hop = sample_rate >= 32000 ? 512 : 256;
     out->peak_threshold = 4.0f;
     out->device = -1;
-    out->min_match = 8;
+    out->min_match = 12;
     out->max_results = 50;
     return AID_OK;
 }
@@ -219,7 +223,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
         return fail(AID_ERR_INVALID, "hop must be one of 128, 256, 512, 1024, 2048");
     if (c.peak_threshold == 0.0f) c.peak_threshold = 4.0f;
     if (!(c.peak_threshold > 0.0f)) return fail(AID_ERR_INVALID, "peak_threshold must be > 0");
-    if (c.min_match <= 0) c.min_match = 8;
+    if (c.min_match <= 0) c.min_match = 12;
     if (c.max_results <= 0) c.max_results = 50;
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -840,9 +844,33 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         for (int q = 0; q < nq; ++q) max_recs = std::max(max_recs, h_count[q]);
     const double per_bucket = e->n_buckets_used > 0 ? (double)e->n_indexed / (double)e->n_buckets_used : 1.0;
     const double votes = std::max(1.0, (double)max_recs * per_bucket);
+    // global histogram: ~2 buckets per expected vote keeps chance buckets >= min_match rare
     int bits = 16;
-    while (bits < 24 && (double)(1ull << bits) < 8.0 * votes) ++bits;
-    for (int attempt = 0; !todo.empty(); ++attempt, bits += 2) {
+    while (bits < 24 && (double)(1ull << bits) < 2.0 * votes) ++bits;
+    // LDS fast path only while its 2^16 counters stay sparse (same load bound)
+    const bool fast = 2.0 * votes <= 65536.0;
+    // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
+    // through to the global-histogram path below
+    if (fast) {
+        {
+            ProfScope ps(e, AID_K_MATCH, s);
+            launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, s);
+        }
+        HIP_TRY(hipGetLastError());
+        std::vector<int32_t> got_n(nq);
+        HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(got_n.data(), e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        std::vector<int> again;
+        for (int q = 0; q < nq; ++q) {
+            if (got_n[q] < 0) again.push_back(q);
+            else nrows[q] = got_n[q];
+        }
+        todo.swap(again);
+        e->n_fallback += (int64_t)todo.size();
+    }
+    for (int attempt = 1; !todo.empty(); ++attempt, bits += 2) {
         if (bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
         const size_t H = (size_t)1 << bits;
         const int batch = (int)std::max<size_t>(1, std::min<size_t>(2048, ((size_t)4 << 30) / (H * 4)));

@@ -134,17 +134,19 @@ struct QueryParams {
     int32_t *nrows;            // [nq]; -1 = LDS table overflow (query not answered)
 };
 
+// one wave per query record; its lanes stride over the record's posting list (coalesced)
 __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
     const int q = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
     const uint32_t hmask = (1u << qp.hist_bits) - 1;
     uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
-    for (int64_t i = a + threadIdx.x; i < z; i += blockDim.x) {
+    for (int64_t i = a + wave; i < z; i += nw) {
         const uint64_t r = qp.recs[i];
         const uint32_t k = key26((uint32_t)r);
         const int32_t tq = (int32_t)(r >> 32);
         const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
-        for (uint32_t p = p0; p < p1; ++p) {
+        for (uint32_t p = p0 + lane; p < p1; p += 64) {
             const uint64_t e = qp.post[p];
             const uint32_t tr = (uint32_t)e;
             if (qp.tomb[tr]) continue;
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
+__global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     __shared__ unsigned long long vkey[kVoteCap];  // (track << 32) | (uint32)d ; ~0 = empty
     __shared__ uint32_t vcnt[kVoteCap], vmin[kVoteCap], vmax[kVoteCap];
     __shared__ uint32_t tkey[kTrackCap];               // track ; ~0 = empty
@@ -180,13 +182,14 @@ __global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
     const uint32_t hmask = (1u << qp.hist_bits) - 1;
     uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
     const uint32_t mm = (uint32_t)qp.min_match;
-    // 1. exact table of candidate votes
-    for (int64_t i = a + tid; i < z; i += blockDim.x) {
+    const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    // 1. exact table of candidate votes (one wave per record, lanes over its postings)
+    for (int64_t i = a + wave; i < z; i += nw) {
         const uint64_t r = qp.recs[i];
         const uint32_t k = key26((uint32_t)r);
         const int32_t tq = (int32_t)(r >> 32);
         const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
-        for (uint32_t p = p0; p < p1; ++p) {
+        for (uint32_t p = p0 + lane; p < p1; p += 64) {
             const uint64_t e = qp.post[p];
             const uint32_t tr = (uint32_t)e;
             if (qp.tomb[tr]) continue;
@@ -269,6 +272,184 @@ __global__ __launch_bounds__(256) void k_vote_final(QueryParams qp) {
     for (int64_t i = tid; i <= (int64_t)hmask; i += blockDim.x) H[i] = 0u;
 }
 
+// ---- K5 (fast path): the whole vote filter in LDS, one 1024-thread workgroup per query ----
+// Phase 1: 2^16 16-bit hashed counters of (track, d) votes (128 KB of LDS); each wave
+//          takes one query record at a time and its 64 lanes stride over that record's
+//          posting list (coalesced 512-byte reads).
+// Phase 2: counters >= min_match -> a 2^16-bit "hot" bitmap (8 KB).
+// Phase 3: the counter region is reused as the exact (track, d) table; only votes whose
+//          bucket is hot are inserted (exact superset filter, as in K5a/K5b).
+// Phase 4: best d per track, rank, write rows (same as K5b). Any table overflow, or a
+//          query too long for 16-bit counters, reports nrows = -1 and the host re-runs it on
+//          the global-histogram path.
+constexpr int kLdsHistBits = 16;
+constexpr int kFastVoteCap = 4096;
+constexpr int kFastTrackCap = 1024;
+constexpr int kFastThreads = 1024;
+
+struct FastLds {
+    union {
+        uint32_t hist[(1 << kLdsHistBits) / 2];  // two 16-bit counters per word
+        struct {
+            unsigned long long vkey[kFastVoteCap];
+            uint32_t vcnt[kFastVoteCap], vmin[kFastVoteCap], vmax[kFastVoteCap];
+            uint32_t tkey[kFastTrackCap];
+            unsigned long long tbest[kFastTrackCap];
+        } t;
+    } u;
+    uint32_t hot[(1 << kLdsHistBits) / 32];
+    int32_t out_n, overflow;
+};
+
+__global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
+    __shared__ FastLds L;  // 136 KB: one workgroup per CU
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = kFastThreads / 64;
+    const int64_t a = qp.qstart[q], n = qp.qcount[q];
+    const uint32_t mm = (uint32_t)qp.min_match;
+    const uint32_t hmask = (1u << kLdsHistBits) - 1;
+    if (n > 30000) {  // 16-bit counters could wrap: let the global path answer
+        if (tid == 0) qp.nrows[q] = -1;
+        return;
+    }
+    for (int i = tid; i < (1 << kLdsHistBits) / 2; i += kFastThreads) L.u.hist[i] = 0u;
+    if (tid == 0) { L.out_n = 0; L.overflow = 0; }
+    __syncthreads();
+    // phase 1
+    for (int64_t i = wave; i < n; i += nw) {
+        const uint64_t r = qp.recs[a + i];
+        const uint32_t k = key26((uint32_t)r);
+        const int32_t tq = (int32_t)(r >> 32);
+        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
+        for (uint32_t p = p0 + lane; p < p1; p += 64) {
+            const uint64_t e = qp.post[p];
+            const uint32_t tr = (uint32_t)e;
+            if (qp.tomb[tr]) continue;
+            const uint32_t h = mix_td(tr, (int32_t)(e >> 32) - tq) & hmask;
+            atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
+        }
+    }
+    __syncthreads();
+    // phase 2
+    for (int w = tid; w < (1 << kLdsHistBits) / 32; w += kFastThreads) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t v = L.u.hist[w * 16 + j];
+            bits |= (uint32_t)((v & 0xFFFFu) >= mm) << (2 * j);
+            bits |= (uint32_t)((v >> 16) >= mm) << (2 * j + 1);
+        }
+        L.hot[w] = bits;
+    }
+    __syncthreads();
+    for (int i = tid; i < kFastVoteCap; i += kFastThreads) {
+        L.u.t.vkey[i] = ~0ull;
+        L.u.t.vcnt[i] = 0;
+        L.u.t.vmin[i] = 0xFFFFFFFFu;
+        L.u.t.vmax[i] = 0;
+    }
+    for (int i = tid; i < kFastTrackCap; i += kFastThreads) {
+        L.u.t.tkey[i] = 0xFFFFFFFFu;
+        L.u.t.tbest[i] = 0ull;
+    }
+    __syncthreads();
+    // phase 3
+    for (int64_t i = wave; i < n; i += nw) {
+        const uint64_t r = qp.recs[a + i];
+        const uint32_t k = key26((uint32_t)r);
+        const int32_t tq = (int32_t)(r >> 32);
+        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
+        for (uint32_t p = p0 + lane; p < p1; p += 64) {
+            const uint64_t e = qp.post[p];
+            const uint32_t tr = (uint32_t)e;
+            if (qp.tomb[tr]) continue;
+            const int32_t d = (int32_t)(e >> 32) - tq;
+            const uint32_t hf = mix_td(tr, d);
+            const uint32_t h = hf & hmask;
+            if (!((L.hot[h >> 5] >> (h & 31)) & 1u)) continue;
+            const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
+            uint32_t s = (hf >> 20) & (kFastVoteCap - 1);
+            int probes = 0;
+            for (;;) {
+                const unsigned long long old = atomicCAS(&L.u.t.vkey[s], ~0ull, key);
+                if (old == ~0ull || old == key) {
+                    atomicAdd(&L.u.t.vcnt[s], 1u);
+                    atomicMin(&L.u.t.vmin[s], (uint32_t)tq);
+                    atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
+                    break;
+                }
+                if (++probes >= kFastVoteCap) { L.overflow = 1; break; }
+                s = (s + 1) & (kFastVoteCap - 1);
+            }
+        }
+    }
+    __syncthreads();
+    // phase 4: best d per track
+    for (int s = tid; s < kFastVoteCap; s += kFastThreads) {
+        if (L.u.t.vkey[s] == ~0ull || L.u.t.vcnt[s] < mm) continue;
+        const uint32_t tr = (uint32_t)(L.u.t.vkey[s] >> 32);
+        const int32_t d = (int32_t)(uint32_t)L.u.t.vkey[s];
+        const unsigned long long packed = ((unsigned long long)L.u.t.vcnt[s] << 32) | (uint32_t)~((uint32_t)d + 0x80000000u);
+        uint32_t t = (tr * 0x9E3779B1u >> 22) & (kFastTrackCap - 1);
+        int probes = 0;
+        for (;;) {
+            const uint32_t old = atomicCAS(&L.u.t.tkey[t], 0xFFFFFFFFu, tr);
+            if (old == 0xFFFFFFFFu || old == tr) {
+                atomicMax(&L.u.t.tbest[t], packed);
+                break;
+            }
+            if (++probes >= kFastTrackCap) { L.overflow = 1; break; }
+            t = (t + 1) & (kFastTrackCap - 1);
+        }
+    }
+    __syncthreads();
+    // phase 5: winning (track, d) rows -> rank -> output (rows staged in the hot bitmap area)
+    int32_t(*rowbuf)[5] = reinterpret_cast<int32_t(*)[5]>(L.hot);  // 8 KB = 409 rows
+    constexpr int kRowCap = (int)(sizeof(L.hot) / (5 * sizeof(int32_t)));
+    for (int s = tid; s < kFastVoteCap; s += kFastThreads) {
+        if (L.u.t.vkey[s] == ~0ull || L.u.t.vcnt[s] < mm) continue;
+        const uint32_t tr = (uint32_t)(L.u.t.vkey[s] >> 32);
+        const int32_t d = (int32_t)(uint32_t)L.u.t.vkey[s];
+        const unsigned long long packed = ((unsigned long long)L.u.t.vcnt[s] << 32) | (uint32_t)~((uint32_t)d + 0x80000000u);
+        uint32_t t = (tr * 0x9E3779B1u >> 22) & (kFastTrackCap - 1);
+        for (int probes = 0; probes < kFastTrackCap && L.u.t.tkey[t] != tr; ++probes) t = (t + 1) & (kFastTrackCap - 1);
+        if (L.u.t.tkey[t] == tr && L.u.t.tbest[t] == packed) {
+            const int o = atomicAdd(&L.out_n, 1);
+            if (o < kRowCap) {
+                rowbuf[o][0] = (int32_t)L.u.t.vcnt[s];
+                rowbuf[o][1] = (int32_t)tr;
+                rowbuf[o][2] = d;
+                rowbuf[o][3] = (int32_t)L.u.t.vmin[s];
+                rowbuf[o][4] = (int32_t)L.u.t.vmax[s];
+            }
+        }
+    }
+    __syncthreads();
+    const int nr = min(L.out_n, kRowCap);
+    for (int i = tid; i < nr; i += kFastThreads) {
+        int rank = 0;
+        for (int j = 0; j < nr; ++j) {
+            const bool before = rowbuf[j][0] > rowbuf[i][0] ||
+                                (rowbuf[j][0] == rowbuf[i][0] && (uint32_t)rowbuf[j][1] < (uint32_t)rowbuf[i][1]);
+            rank += before ? 1 : 0;
+        }
+        if (rank < qp.max_rows) {
+            int32_t *o = qp.rows + ((int64_t)q * qp.max_rows + rank) * 5;
+#pragma unroll
+            for (int c = 0; c < 5; ++c) o[c] = rowbuf[i][c];
+        }
+    }
+    if (tid == 0) qp.nrows[q] = (L.overflow || L.out_n > kRowCap) ? -1 : min(nr, qp.max_rows);
+}
+
+void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
+                      const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
+                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, hipStream_t s) {
+    if (nq <= 0) return;
+    QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows};
+    hipLaunchKernelGGL(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
+}
+
 void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
                         uint32_t *cnt, hipStream_t s) {
     if (n <= 0) return;
@@ -303,7 +484,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
                    nrows};
     hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
-    hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(256), 0, s, qp);
+    hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
 
 // number of non-empty buckets (for the query histogram sizing)

@@ -85,6 +85,7 @@ def main() -> int:
     fp_hits = 0
     off_err = []
     neg_best = []
+    pos_best = []
     for q in range(nq):
         windows = []
         for w in range(3):
@@ -95,6 +96,7 @@ def main() -> int:
             windows.append(ms)
         ranked = ex.rank(ex.consensus_score(windows), 10)
         if q < n_pos:
+            pos_best.append(max((int(all_rows[3 * q + w][0, 0]) if len(all_rows[3 * q + w]) else 0) for w in range(3)))
             if ranked and ranked[0].track_uuid.int - 1 == int(truth[q]):
                 top1 += 1
                 off_err.append(abs(ranked[0].offset_seconds - (starts[q] / args.sr + 0.75)))
@@ -113,6 +115,7 @@ def main() -> int:
         "median_offset_error_s": round(float(np.median(off_err)), 4) if off_err else None,
         "engine_min_match": eng.min_match,
         "neg_best_window_count_pcts": [int(np.percentile(neg_best, p)) for p in (50, 90, 99)] if neg_best else None,
+        "pos_best_window_count_pcts": [int(np.percentile(pos_best, p)) for p in (1, 10, 50)] if pos_best else None,
         "gpu_s": round(t_gpu, 3), "host_consensus_s": round(t_host, 3), "index_build_s": round(t_index, 3),
         "index_tracks": args.tracks, "index_postings": st.postings_total, "data": "synthetic",
     }), flush=True)

@@ -52,7 +52,7 @@ typedef struct aid_config {
     int32_t hop;           /* 0 = FPSPEC default: 512 at sr >= 32 kHz, else 256 */
     float peak_threshold;  /* 0 = FPSPEC default 4.0 */
     int32_t device;        /* HIP device ordinal; -1 = current device */
-    int32_t min_match;     /* query: 0 = FPSPEC default 8 */
+    int32_t min_match;     /* query: 0 = FPSPEC default 12 */
     int32_t max_results;   /* query: 0 = FPSPEC default 50 */
     int32_t reserved[10];
 } aid_config;

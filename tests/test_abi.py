@@ -32,7 +32,7 @@ def test_abi_version_and_defaults_without_gpu():
     assert L.aid_abi_version() == 1
     cfg = _lib.AidConfig()
     assert L.aid_config_default(44100, ctypes.byref(cfg)) == 0
-    assert (cfg.hop, cfg.min_match, cfg.max_results) == (512, 8, 50)
+    assert (cfg.hop, cfg.min_match, cfg.max_results) == (512, 12, 50)
     assert abs(cfg.peak_threshold - 4.0) < 1e-9
     assert L.aid_config_default(16000, ctypes.byref(cfg)) == 0 and cfg.hop == 256
     assert L.aid_config_default(0, ctypes.byref(cfg)) == _lib.AID_ERR_INVALID
