@@ -402,7 +402,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
             ProfScope ps(e, AID_K_PEAKS, s);
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, e->cfg.peak_threshold, e->mask.p, s);
         }
-        {
+        if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
                              false, s);

@@ -12,10 +12,11 @@
 //   3. gives each thread a contiguous run of anchors; a thread walks forward from
 //      each anchor while t2 - t1 <= 63 and keeps the first 10 targets with
 //      |k2 - k1| <= 127.
-// Pass COUNT writes the chunk's record total; pass WRITE re-derives its base from
-// the totals of the clip's earlier chunks, block-scans per-thread totals and
-// stores records {hash, t1} in canonical order. Chunk 0 of a clip also writes
-// the clip's record count.
+// Pass COUNT writes the chunk's record total (only clips with more than one chunk
+// need it; the host skips the launch when none has); pass WRITE re-derives its base
+// from the totals of the clip's earlier chunks, block-scans per-thread totals and
+// stores records {hash, t1} in canonical order. Chunk 0 of a clip also writes the
+// clip's record count.
 #include "aidfp_device.h"
 
 namespace aid {
@@ -82,6 +83,8 @@ __global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ 
     const int64_t g1 = min(c1 + (int64_t)kZoneDT, F);
     const int nf = (int)(g1 - c0);
     const uint64_t *Mc = mask + (cd.frame_base + c0) * kMaskWords;
+    const int64_t nck = (F + kHashChunk - 1) / kHashChunk;
+    if (!WRITE && nck == 1) return;  // single-chunk clips: the WRITE pass needs no base
 
     // 1. per-frame counts over a contiguous run of frames per thread, block scan
     const int per = (nf + 255) / 256;
@@ -142,18 +145,21 @@ __global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ 
     if constexpr (!WRITE) {
         if (tid == 0) chunk_counts[chunk] = chunk_total;
     } else {
-        // base of this chunk inside the clip = sum of the clip's earlier chunks
-        int64_t pre = 0;
-        for (int64_t c = cd.chunk_base + tid; c < chunk; c += 256) pre += chunk_counts[c];
         int64_t before = 0;
-        block_excl_scan(pre, scan_tmp, &before);
-        if (q == 0) {
-            int64_t all = 0;
-            const int64_t nck = (F + kHashChunk - 1) / kHashChunk;
-            for (int64_t c = cd.chunk_base + tid; c < cd.chunk_base + nck; c += 256) all += chunk_counts[c];
-            int64_t tot = 0;
-            block_excl_scan(all, scan_tmp, &tot);
-            if (tid == 0) clip_counts[lo] = tot;
+        if (nck == 1) {
+            if (tid == 0) clip_counts[lo] = chunk_total;
+        } else {
+            // base of this chunk inside the clip = sum of the clip's earlier chunks
+            int64_t pre = 0;
+            for (int64_t c = cd.chunk_base + tid; c < chunk; c += 256) pre += chunk_counts[c];
+            block_excl_scan(pre, scan_tmp, &before);
+            if (q == 0) {
+                int64_t all = 0;
+                for (int64_t c = cd.chunk_base + tid; c < cd.chunk_base + nck; c += 256) all += chunk_counts[c];
+                int64_t tot = 0;
+                block_excl_scan(all, scan_tmp, &tot);
+                if (tid == 0) clip_counts[lo] = tot;
+            }
         }
         uint64_t *out = records + cd.hash_base + before + excl;
         int64_t o = 0;

@@ -27,7 +27,10 @@
 
 // AID_K1_DIAG selects a timing-only variant for LDS-conflict attribution (wrong results):
 //   1 = E3 writes lane-contiguous, 2 = real-split mirror reads lane-contiguous,
-//   4 = E1 read lane-contiguous, 5 = E2 read lane-contiguous
+//   4 = E1 read lane-contiguous, 5 = E2 read lane-contiguous,
+//   6 = no E1 exchange, 7 = no E2 exchange, 8 = no E3 exchange (real split on registers),
+//   9 = no stage A/B DFT16 arithmetic, 10 = one float stored per lane and frame (not 16 rows),
+//   11 = no LDS table reads (constant twiddles/window)
 #ifndef AID_K1_DIAG
 #define AID_K1_DIAG 0
 #endif
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #pragma unroll
                 for (int n1 = 0; n1 < 16; ++n1) {
                     const float2 x = ring[(n1 + ROWS * p) & 15];
-                    const float2 w = s_win[64 * n1 + lane];
+                    const float2 w = AID_K1_DIAG == 11 ? make_float2(0.5f, 0.25f) : s_win[64 * n1 + lane];
                     v[n1] = make_float2(x.x * w.x, x.y * w.y);
                 }
                 // the rows just consumed (n1 < ROWS) are replaced by frame f+1's new rows
@@ -102,31 +105,35 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         ring[(ROWS * p + j) & 15] = src[(int64_t)(f + 1) * HOP2 + 64 * (16 - ROWS + j)];
                 }
                 // stage A: lane = n2
-                dft16(v, t16);
+                if (AID_K1_DIAG != 9) dft16(v, t16);
                 // T1K[n2*k1]; lane 0 multiplies by T1K[0] = (1,-0): value-identical (FPSPEC 4 note)
 #pragma unroll
-                for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], s_ta[64 * k1 + lane]);
+                for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], AID_K1_DIAG == 11 ? t16[k1 % 10] : s_ta[64 * k1 + lane]);
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
+                if (AID_K1_DIAG != 6) {
 #pragma unroll
-                for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 68 + lane] = v[k1];
-                wave_lds_sync();
+                    for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 68 + lane] = v[k1];
+                    wave_lds_sync();
 #pragma unroll
-                for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[AID_K1_DIAG == 4 ? m1 * 68 + lane : kq * 68 + 4 * m1 + mq];
-                wave_lds_sync();
+                    for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[AID_K1_DIAG == 4 ? m1 * 68 + lane : kq * 68 + 4 * m1 + mq];
+                    wave_lds_sync();
+                }
                 // stage B
-                dft16(v, t16);
+                if (AID_K1_DIAG != 9) dft16(v, t16);
 #pragma unroll
-                for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], s_tb[64 * j1 + lane]);
+                for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], AID_K1_DIAG == 11 ? t16[j1 % 10] : s_tb[64 * j1 + lane]);
                 // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
+                if (AID_K1_DIAG != 7) {
 #pragma unroll
-                for (int j1 = 0; j1 < 16; ++j1) buf[lane * 17 + j1] = v[j1];
-                wave_lds_sync();
+                    for (int j1 = 0; j1 < 16; ++j1) buf[lane * 17 + j1] = v[j1];
+                    wave_lds_sync();
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
+                    for (int r = 0; r < 4; ++r)
 #pragma unroll
-                    for (int m2 = 0; m2 < 4; ++m2)
-                        v[4 * r + m2] = buf[AID_K1_DIAG == 5 ? (4 * r + m2) * 68 + lane : (4 * kq + m2) * 17 + mq + 4 * r];
-                wave_lds_sync();
+                        for (int m2 = 0; m2 < 4; ++m2)
+                            v[4 * r + m2] = buf[AID_K1_DIAG == 5 ? (4 * r + m2) * 68 + lane : (4 * kq + m2) * 17 + mq + 4 * r];
+                    wave_lds_sync();
+                }
                 // stage C: DFT4 over m2 -> Z[kq + 16*(mq + 4r) + 256*j2]; E3 natural order, pad 1 per 32
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -134,11 +141,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #pragma unroll
                     for (int j2 = 0; j2 < 4; ++j2) {
                         const int k = AID_K1_DIAG == 1 ? lane + 64 * (r + 4 * j2) : kq + 16 * (mq + 4 * r) + 256 * j2;
-                        buf[e3(k)] = v[4 * r + j2];
+                        if (AID_K1_DIAG != 8) buf[e3(k)] = v[4 * r + j2];
                     }
                 }
                 wave_lds_sync();
                 float *drow = dst + (int64_t)f * kBins;
+                float acc10 = 0.f;
                 // real split, bins in mirror pairs (k, 1024-k): one read of Z[k], Z[1024-k] serves
                 // both. For bin 1024-k the FPSPEC sums are the same exact values with signs
                 // flipped (a+c, c+a commute; b-d = -(d-b)), so both bins stay bit-exact.
@@ -146,25 +154,28 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 for (int i = 0; i < 8; ++i) {
                     const int k = lane + 64 * i;  // 0..511
                     const int kk = (1024 - k) & 1023;
-                    const float2 a = buf[e3(k)];
-                    const float2 b = buf[e3(AID_K1_DIAG == 2 ? (k ^ 512) : kk)];
+                    const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[e3(k)];
+                    const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[e3(AID_K1_DIAG == 2 ? (k ^ 512) : kk)];
                     const float er = a.x + b.x, ei = a.y - b.y;
                     const float orr = a.y + b.y, oi = b.x - a.x;
                     {
-                        const float2 tw = cmul(make_float2(orr, oi), s_t2k[k]);
+                        const float2 tw = cmul(make_float2(orr, oi), AID_K1_DIAG == 11 ? t16[i] : s_t2k[k]);
                         const float xr = er + tw.x, xi = ei + tw.y;
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                         if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
+                        else if (AID_K1_DIAG == 10) acc10 += P;
                         else drow[k] = P;
                     }
                     if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
-                        const float2 tw = cmul(make_float2(orr, -oi), s_t2k[1024 - k]);
+                        const float2 tw = cmul(make_float2(orr, -oi), AID_K1_DIAG == 11 ? t16[i + 1] : s_t2k[1024 - k]);
                         const float xr = er + tw.x, xi = -ei + tw.y;
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                         if constexpr (LOGMAG) drow[1024 - k] = 10.0f * log10f(P + 1e-10f);
+                        else if (AID_K1_DIAG == 10) acc10 += P;
                         else drow[1024 - k] = P;
                     }
                 }
+                if (AID_K1_DIAG == 10) drow[lane] = acc10;
                 if (lane == 0) {  // bin 512 pairs with itself
                     const float2 a = buf[e3(512)];
                     const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;

@@ -151,7 +151,7 @@ def main() -> int:
 
     kern = {k: {"ms_per_launch": (ms / cnt if cnt else None), "launches": cnt} for k, (ms, cnt) in prof.items() if cnt}
     alg = algorithmic_bytes(frames, CLIPS * n)
-    dom = max(("stft_power", "peak_pick"), key=lambda k: kern.get(k, {}).get("ms_per_launch") or 0.0)
+    dom = max(("stft_power", "peak_pick"), key=lambda k: (kern.get(k) or {}).get("ms_per_launch") or 0.0)
     dom_ms = kern[dom]["ms_per_launch"]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
     pmc, pmc_src = load_pmc(dom)
