@@ -6,15 +6,15 @@
 //
 // One workgroup streams one strip of kPeakStrip output frames of one clip and
 // reads every power row of the strip (+7 halo rows each side) once:
-//   * thread j owns bins 4j..4j+3 (one float4 load per row), prefetched 8 rows
-//     ahead in a register ring (~64 KB of loads in flight per CU);
+//   * thread j owns bins 4j..4j+3 (one float4 load per row); the next batch of 4
+//     rows is in flight in registers while the current one is processed;
 //   * rows are staged in LDS 4 at a time (double-buffered, one barrier per 4
 //     rows); each thread reads its +-15-bin neighbours from LDS;
-//   * the vertical +-7-frame part is register-resident: `before` is complete when a
-//     row arrives (the previous 7 rows' row-max live in an 8-slot register ring); a
-//     candidate then stays pending until each of the next 7 rows' row-max has been
-//     checked against it (<= keeps it, > knocks it out); ring slots are compile-time
-//     because the row loop is unrolled by 8;
+//   * the vertical +-7-frame part is register-resident: one sliding maximum M7 of the
+//     row-max over the last 7 rows (from an 8-slot ring of pair maxima, 4 VALU/bin)
+//     gives both `before` of the arriving row (the previous M7, strict) and `after` of
+//     the row 7 back (the current M7, non-strict), whose candidate power waits in an
+//     8-slot ring; ring slots are compile-time because the row loop is unrolled by 8;
 //   * a decided row is emitted with 4 wave ballots (one per bin offset i < 4): mask
 //     word 4*w + i of a frame holds, at bit l, the peak flag of bin 256*w + 4*l + i
 //     ("ballot layout"; K3 and aidfp.engine.peaks_from_mask unshuffle it).
@@ -25,8 +25,11 @@
 namespace aid {
 
 constexpr int kRowsPerStep = 4;
+#ifndef AID_K2_MIN_WAVES
+#define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
+#endif
 
-__global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
+__global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, float thr,
                                                   uint64_t *__restrict__ mask) {
     __shared__ __attribute__((aligned(16))) float rows[2][kRowsPerStep][kBins + 32];
@@ -64,22 +67,29 @@ __global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ pow
             }
     }
 
-    float fh[8][4];    // row-max (Full) of recent rows, slot = iteration & 7
-    float pend[8][4];  // power of pending candidates not yet beaten by a later row (-1 = none)
+    // vertical +-7 as one sliding max: M7(s) = max row-max (fm) over rows s-6..s, built from
+    // pair maxima m2[s] = max(fm[s], fm[s-1]) as max(m2[s], m2[s-2], m2[s-4], m2[s-5]).
+    // `before` of row s is M7(s-1) (strict), `after` of row s-7 is M7(s) (non-strict).
+    float m2r[8][4];   // pair maxima, slot = iteration & 7
+    float pend[8][4];  // power of this row's candidates (-1 = none), decided 7 rows later
+    float fprev[4], m7p[4];
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { fh[s][i] = 0.f; pend[s][i] = -1.f; }
-    const float kmin_ok = (tid == 0) ? 0.f : 1.f;  // bin 0 is never a peak
+        for (int i = 0; i < 4; ++i) { m2r[s][i] = 0.f; pend[s][i] = -1.f; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { fprev[i] = 0.f; m7p[i] = 0.f; }
+    // bin 0 is never a peak: its `before` bound is +inf
+    const float kmin_pen = (tid == 0) ? __builtin_huge_valf() : 0.f;
 
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
     const int64_t rbeg = t0 - kPeakDT;
     const int iters = (int)(t1 - t0) + 2 * kPeakDT;
-    float4 pf[8];  // row rbeg+it lives in pf[it & 7]
+    float4 pf[kRowsPerStep];  // rows of the next batch, in flight
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        const int64_t r = rbeg + s;
-        pf[s] = (s < iters && r >= 0 && r < F) ? reinterpret_cast<const float4 *>(P + r * kBins)[tid]
+    for (int j = 0; j < kRowsPerStep; ++j) {
+        const int64_t r = rbeg + j;
+        pf[j] = (j < iters && r >= 0 && r < F) ? reinterpret_cast<const float4 *>(P + r * kBins)[tid]
                                                : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
@@ -90,13 +100,15 @@ __global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ pow
             if (it >= iters) break;  // workgroup-uniform
             const int buf = (it / kRowsPerStep) & 1;
             if (s % kRowsPerStep == 0) {
-                // stage rows it .. it+3 and refill their prefetch slots with rows it+8 .. it+11
+                // stage rows it .. it+3, then fetch rows it+4 .. it+7 (register staging beats
+                // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll
                 for (int j = 0; j < kRowsPerStep; ++j) {
-                    reinterpret_cast<float4 *>(&rows[buf][j][16])[tid] = pf[s + j];
-                    const int64_t rn = rbeg + it + j + 8;
-                    pf[s + j] = (it + j + 8 < iters && rn < F) ? reinterpret_cast<const float4 *>(P + rn * kBins)[tid]
-                                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+                    reinterpret_cast<float4 *>(&rows[buf][j][16])[tid] = pf[j];
+                    const int64_t rn = rbeg + it + j + kRowsPerStep;
+                    pf[j] = (it + j + kRowsPerStep < iters && rn >= 0 && rn < F)
+                                ? reinterpret_cast<const float4 *>(P + rn * kBins)[tid]
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
                 __syncthreads();
             }
@@ -128,28 +140,24 @@ __global__ __launch_bounds__(256) void k_peak_pick(const float *__restrict__ pow
             R[3] = fmaxf(fmaxf(midR, q[32]), fmaxf(q[33], q[34]));
 
             // candidates only inside the strip's output rows (uniform)
-            const float row_ok = (r >= t0 && r < t1) ? 1.f : 0.f;
+            // (rows outside get threshold +inf)
+            const float thr_row = (r >= t0 && r < t1) ? thr : __builtin_huge_valf();
             bool pk[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float p = q[16 + i];
                 const float fm = fmaxf(fmaxf(L[i], p), R[i]);
-                float bf = fmaxf(L[i], thr);
-#pragma unroll
-                for (int d = 1; d <= 7; ++d) bf = fmaxf(bf, fh[(s - d) & 7][i]);
-                const float okf = (i == 0 ? kmin_ok : 1.f) * row_ok;
-                // `after` part of this row: the right window (p >= R); later rows test below
-                const bool cand = (p > bf) & (p >= R[i]) & (okf > 0.f);
-                // this row's Full knocks out pending candidates of rows r-1 .. r-7 it exceeds
-#pragma unroll
-                for (int d = 1; d <= 7; ++d) {
-                    float &pe = pend[(s - d) & 7][i];
-                    pe = (fm <= pe) ? pe : -1.f;
-                }
-                // row r-7 (slot s-7 == s+1) has now met all 7 later rows
-                pk[i] = pend[(s + 1) & 7][i] >= 0.f;
-                fh[s][i] = fm;
-                pend[s][i] = cand ? p : -1.f;
+                const float m2 = fmaxf(fm, fprev[i]);
+                fprev[i] = fm;
+                m2r[s][i] = m2;
+                const float m7 = fmaxf(fmaxf(fmaxf(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
+                const float bf = fmaxf(fmaxf(i == 0 ? fmaxf(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
+                m7p[i] = m7;
+                // candidate: p > before (strict) and p >= right window; power >= 0, so -1 = none
+                const float c1 = (p > bf) ? p : -1.f;
+                // row r-7 (slot s+1) has now met all 7 later rows: p >= their row-max
+                pk[i] = pend[(s + 1) & 7][i] >= m7;
+                pend[s][i] = (c1 >= R[i]) ? c1 : -1.f;
             }
             const uint64_t b0 = __ballot(pk[0]), b1 = __ballot(pk[1]), b2 = __ballot(pk[2]), b3 = __ballot(pk[3]);
             const int64_t rd = r - kPeakDT;
