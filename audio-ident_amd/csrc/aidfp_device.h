@@ -65,6 +65,19 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10]) 
 }
 
 // compiler + hardware ordering point for wave-private LDS exchanges
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Orders a wave's own LDS exchange (write -> read by other lanes of the SAME wave). A wave's
+// LDS instructions are executed in issue order (LLVM AMDGPU memory model: LDS accesses of one
+// wavefront stay in order), so only the compiler must be kept from moving accesses across; the
+// s_waitcnt form (AID_K1_LDS_WAIT=1) additionally stalls the wave for a full round trip.
+#ifndef AID_K1_LDS_WAIT
+#define AID_K1_LDS_WAIT 0
+#endif
+__device__ __forceinline__ void wave_lds_sync() {
+#if AID_K1_LDS_WAIT
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+    asm volatile("" ::: "memory");
+#endif
+}
 
 }  // namespace aid

@@ -21,7 +21,8 @@
 //     (E3), then the real split reads each mirror pair (Z[k], Z[1024-k]) once
 //     (conflict-free) and produces both bins; stores are 64 consecutive bins per
 //     wave-instruction (the mirror bins in descending order, same 256-B segment).
-// A workgroup is 12 waves (3 per SIMD) sharing 32 KB of tables in LDS; the
+// A workgroup is 12 waves (3 per SIMD) sharing 32 KB of tables in LDS (float4 pairs,
+// read with ds_read_b128); the
 // exchanges are wave-private, so there is no workgroup barrier in the loop.
 #include "aidfp_device.h"
 
@@ -29,8 +30,7 @@
 //   1 = E3 writes lane-contiguous, 2 = real-split mirror reads lane-contiguous,
 //   4 = E1 read lane-contiguous, 5 = E2 read lane-contiguous,
 //   6 = no E1 exchange, 7 = no E2 exchange, 8 = no E3 exchange (real split on registers),
-//   9 = no stage A/B DFT16 arithmetic, 10 = one float stored per lane and frame (not 16 rows),
-//   11 = no LDS table reads (constant twiddles/window)
+//   9 = no stage A/B DFT16 arithmetic, 10 = one float stored per lane and frame (not 16 rows)
 #ifndef AID_K1_DIAG
 #define AID_K1_DIAG 0
 #endif
@@ -51,20 +51,30 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68, E2: 64 x 17, E3: 1024
-    __shared__ float2 s_win[1024], s_ta[1024], s_t2k[1024], s_tb[1024];
+    // tables as float4 pairs [h][lane], one ds_read_b128 per pair (hipcc would otherwise merge the
+    // stride-512-B float2 reads into ds_read2st64_b64, which costs the LDS twice the cycles):
+    //   s_win4[h] = window of rows 2h, 2h+1 ; s_ta4[h] = T1K[lane*k1], k1 = 2h, 2h+1
+    //   s_tb4[h] = T64[(lane&3)*j1], j1 = 2h, 2h+1 ; s_t2p[i] = (T2K[k], T2K[1024-k]), k = lane + 64i
+    __shared__ float4 s_win4[512], s_ta4[512], s_tb4[512], s_t2p[512];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     float2 *buf = lds[wave];
     const int kq = lane >> 2;  // stage B/C: k1
     const int mq = lane & 3;   // stage B: m2 ; stage C: s
 
-    for (int i = threadIdx.x; i < 1024; i += kStftWaves * 64) {
-        s_win[i] = tab->win2[i];
-        s_t2k[i] = tab->t2k[i];
-        const int k1 = i >> 6, l = i & 63;
-        s_ta[i] = tab->t1k[l * k1];          // [k1][lane] = T1K[lane*k1]
-        s_tb[i] = tab->t64[(l & 3) * k1];    // [j1][lane] = T64[m2*j1], m2 = lane & 3
+    for (int i = threadIdx.x; i < 512; i += kStftWaves * 64) {
+        const int h = i >> 6, l = i & 63, a = 2 * h, b = 2 * h + 1;
+        const float2 w0 = tab->win2[64 * a + l], w1 = tab->win2[64 * b + l];
+        s_win4[i] = make_float4(w0.x, w0.y, w1.x, w1.y);
+        const float2 ta0 = tab->t1k[l * a], ta1 = tab->t1k[l * b];
+        s_ta4[i] = make_float4(ta0.x, ta0.y, ta1.x, ta1.y);
+        const float2 tb0 = tab->t64[(l & 3) * a], tb1 = tab->t64[(l & 3) * b];
+        s_tb4[i] = make_float4(tb0.x, tb0.y, tb1.x, tb1.y);
+        const int k = l + 64 * h;
+        const float2 c0 = tab->t2k[k], c1 = tab->t2k[(1024 - k) & 1023];  // k = 0: mirror unused
+        s_t2p[i] = make_float4(c0.x, c0.y, c1.x, c1.y);
     }
+    const float2 t512 = tab->t2k[512];
     float2 t16[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) t16[i] = tab->t16[i];
@@ -93,10 +103,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
             if (f < nfr) {  // wave-uniform
                 float2 v[16];
 #pragma unroll
-                for (int n1 = 0; n1 < 16; ++n1) {
-                    const float2 x = ring[(n1 + ROWS * p) & 15];
-                    const float2 w = AID_K1_DIAG == 11 ? make_float2(0.5f, 0.25f) : s_win[64 * n1 + lane];
-                    v[n1] = make_float2(x.x * w.x, x.y * w.y);
+                for (int h = 0; h < 8; ++h) {
+                    const float4 w = s_win4[64 * h + lane];
+                    const float2 x0 = ring[(2 * h + ROWS * p) & 15], x1 = ring[(2 * h + 1 + ROWS * p) & 15];
+                    v[2 * h] = make_float2(x0.x * w.x, x0.y * w.y);
+                    v[2 * h + 1] = make_float2(x1.x * w.z, x1.y * w.w);
                 }
                 // the rows just consumed (n1 < ROWS) are replaced by frame f+1's new rows
                 if (f + 1 < nfr) {
@@ -108,7 +119,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 if (AID_K1_DIAG != 9) dft16(v, t16);
                 // T1K[n2*k1]; lane 0 multiplies by T1K[0] = (1,-0): value-identical (FPSPEC 4 note)
 #pragma unroll
-                for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], AID_K1_DIAG == 11 ? t16[k1 % 10] : s_ta[64 * k1 + lane]);
+                for (int h = 0; h < 8; ++h) {
+                    const float4 t = s_ta4[64 * h + lane];
+                    if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
+                    v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
+                }
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
                 if (AID_K1_DIAG != 6) {
 #pragma unroll
@@ -121,7 +136,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 // stage B
                 if (AID_K1_DIAG != 9) dft16(v, t16);
 #pragma unroll
-                for (int j1 = 1; j1 < 16; ++j1) v[j1] = cmul(v[j1], AID_K1_DIAG == 11 ? t16[j1 % 10] : s_tb[64 * j1 + lane]);
+                for (int h = 0; h < 8; ++h) {
+                    const float4 t = s_tb4[64 * h + lane];
+                    if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
+                    v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
+                }
                 // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
                 if (AID_K1_DIAG != 7) {
 #pragma unroll
@@ -158,8 +177,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[e3(AID_K1_DIAG == 2 ? (k ^ 512) : kk)];
                     const float er = a.x + b.x, ei = a.y - b.y;
                     const float orr = a.y + b.y, oi = b.x - a.x;
+                    const float4 t2 = s_t2p[64 * i + lane];
                     {
-                        const float2 tw = cmul(make_float2(orr, oi), AID_K1_DIAG == 11 ? t16[i] : s_t2k[k]);
+                        const float2 tw = cmul(make_float2(orr, oi), make_float2(t2.x, t2.y));
                         const float xr = er + tw.x, xi = ei + tw.y;
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                         if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
@@ -167,7 +187,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         else drow[k] = P;
                     }
                     if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
-                        const float2 tw = cmul(make_float2(orr, -oi), AID_K1_DIAG == 11 ? t16[i + 1] : s_t2k[1024 - k]);
+                        const float2 tw = cmul(make_float2(orr, -oi), make_float2(t2.z, t2.w));
                         const float xr = er + tw.x, xi = -ei + tw.y;
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                         if constexpr (LOGMAG) drow[1024 - k] = 10.0f * log10f(P + 1e-10f);
@@ -179,7 +199,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 if (lane == 0) {  // bin 512 pairs with itself
                     const float2 a = buf[e3(512)];
                     const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
-                    const float2 tw = cmul(make_float2(orr, oi), s_t2k[512]);
+                    const float2 tw = cmul(make_float2(orr, oi), t512);
                     const float xr = er + tw.x, xi = ei + tw.y;
                     const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                     if constexpr (LOGMAG) drow[512] = 10.0f * log10f(P + 1e-10f);
