@@ -71,7 +71,10 @@ struct DevBuf {
     size_t n = 0;  // capacity in elements
     hipError_t reserve(size_t want) {
         if (want <= n) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) {  // growing: in-flight work of earlier calls may still use the old buffer
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+        }
         p = nullptr;
         n = 0;
         size_t cap = std::max(want, (size_t)1);
@@ -134,6 +137,12 @@ struct aid_engine {
 
     ClipDesc *h_desc = nullptr;  // pinned
     size_t h_desc_cap = 0;
+    // extraction call hazards, tracked with events instead of a stream sync per call:
+    // h_desc is the source of an async H2D copy; pcm_stage is read by K1
+    hipEvent_t desc_ev = nullptr, stage_ev = nullptr;
+    bool desc_ev_live = false, stage_ev_live = false;
+    std::vector<int64_t> desc_key;  // offsets (+ pcm location) the device descriptors were built for
+    ClipDesc *desc_dev_for_key = nullptr;
     std::vector<int64_t> clip_base;  // host copy of desc[c].hash_base
     std::vector<int64_t> clip_frames;
     int n_clips = 0;
@@ -301,6 +310,8 @@ void aid_engine_destroy(aid_engine *e) {
     e->x_dst.release();
     e->x_tracks.release();
     if (e->h_desc) (void)hipHostFree(e->h_desc);
+    if (e->desc_ev) (void)hipEventDestroy(e->desc_ev);
+    if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
     if (e->d_tab) (void)hipFree(e->d_tab);
     if (e->d_sin) (void)hipFree(e->d_sin);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -337,11 +348,21 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         HIP_TRY(hipHostMalloc((void **)&e->h_desc, sizeof(ClipDesc) * ((size_t)n_clips + 1)));
         e->h_desc_cap = (size_t)n_clips + 1;
     }
-    // host PCM staging goes through the previous call's buffers: make sure they are idle
-    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    // a different stream than the previous call's: order against it the simple way
+    if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    // same offsets and PCM location as the descriptors already on the device: no re-upload
+    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() == (size_t)n_clips + 2 &&
+                     e->desc_key[n_clips + 1] == loc;
+    for (int c = 0; desc_same && c <= n_clips; ++c) desc_same = e->desc_key[c] == offsets[c];
+    // h_desc is rewritten below: the previous descriptor upload must have left it
+    if (e->desc_ev_live) {
+        HIP_TRY(hipEventSynchronize(e->desc_ev));
+        e->desc_ev_live = false;
+    }
     e->clip_base.assign(n_clips, 0);
     e->clip_frames.assign(n_clips, 0);
     int64_t frames = 0, strips = 0, chunks = 0, recs = 0, staged = 0, kstrips = 0;
+    bool empty_clip = false;  // a clip without frames gets no count from K3: zero the counts first
     for (int c = 0; c < n_clips; ++c) {
         const int64_t n = offsets[c + 1] - offsets[c];
         const int64_t F = num_frames(n, hop);
@@ -362,6 +383,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         d.stft_base = kstrips;
         e->clip_base[c] = recs;
         e->clip_frames[c] = F;
+        empty_clip |= F == 0;
         frames += F;
         strips += (F + kPeakStrip - 1) / kPeakStrip;
         chunks += (F + kHashChunk - 1) / kHashChunk;
@@ -376,6 +398,10 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
     HIP_TRY(e->counts.reserve((size_t)n_clips + 1));
     const float *dpcm = pcm;
     if (loc == AID_PCM_HOST && staged > 0) {
+        if (e->stage_ev_live) {  // K1 of an earlier call may still read the staging buffer
+            HIP_TRY(hipEventSynchronize(e->stage_ev));
+            e->stage_ev_live = false;
+        }
         HIP_TRY(e->pcm_stage.reserve((size_t)staged));
         for (int c = 0; c < n_clips; ++c) {
             const int64_t n = offsets[c + 1] - offsets[c];
@@ -385,9 +411,16 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         }
         dpcm = e->pcm_stage.p;
     }
-    if (n_clips > 0)
+    if (n_clips > 0 && !desc_same) {
+        if (!e->desc_ev) HIP_TRY(hipEventCreateWithFlags(&e->desc_ev, hipEventDisableTiming));
         HIP_TRY(hipMemcpyAsync(e->desc.p, e->h_desc, sizeof(ClipDesc) * n_clips, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(e->counts.p, 0, sizeof(int64_t) * ((size_t)n_clips + 1), s));
+        HIP_TRY(hipEventRecord(e->desc_ev, s));
+        e->desc_ev_live = true;
+        e->desc_key.assign(offsets, offsets + n_clips + 1);
+        e->desc_key.push_back(loc);
+        e->desc_dev_for_key = e->desc.p;
+    }
+    if (empty_clip || frames == 0) HIP_TRY(hipMemsetAsync(e->counts.p, 0, sizeof(int64_t) * ((size_t)n_clips + 1), s));
     e->n_clips = n_clips;
     e->total_frames = frames;
     e->total_strips = strips;
@@ -397,6 +430,11 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         {
             ProfScope ps(e, AID_K_STFT, s);
             launch_stft_power(dpcm, e->desc.p, n_clips, kstrips, hop, e->d_tab, e->power.p, false, s);
+        }
+        if (loc == AID_PCM_HOST) {
+            if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(e->stage_ev, s));
+            e->stage_ev_live = true;
         }
         {
             ProfScope ps(e, AID_K_PEAKS, s);

@@ -93,3 +93,45 @@ def test_logmag_tolerance(gpu_engine):
     assert (np.abs(m - m64) / m64.max(axis=1, keepdims=True)).max() <= 1e-4
     sel = P64 >= 1e-6 * P64.max(axis=1, keepdims=True)
     assert np.abs(L - L64)[sel].max() <= 1e-4 * 60.0
+
+
+def test_back_to_back_calls_without_sync(gpu_engine):
+    """aid_extract orders calls with events, not a stream sync per call: changed offsets,
+    repeated offsets (cached descriptors), host/device PCM switches and empty clips
+    queued back to back must each give the oracle's hashes."""
+    import torch
+
+    a = [_clip(40 + i, n, start=31 * i) for i, n in enumerate([44100 * 3, 30000, 44100 * 2])]
+    b = [_clip(50 + i, n, start=17 * i) for i, n in enumerate([44100, 1000, 44100 * 4, 2048])]
+    ref_a = [O.fingerprint(x, HOP) for x in a]
+    ref_b = [O.fingerprint(x, HOP) for x in b]
+
+    def dev(clips):
+        offs = np.zeros(len(clips) + 1, np.int64)
+        for i, x in enumerate(clips):
+            offs[i + 1] = offs[i] + ((len(x) + 1) & ~1)
+        buf = torch.zeros(int(offs[-1]), dtype=torch.float32, device="cuda")
+        for i, x in enumerate(clips):
+            buf[int(offs[i]):int(offs[i]) + len(x)] = torch.from_numpy(x)
+        return buf, offs
+
+    da, oa = dev(a)
+    db, ob = dev(b)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):  # a, b, a again (cache key flips), queued without syncs
+        gpu_engine.extract_device(da.data_ptr(), oa, s)
+        gpu_engine.extract_device(db.data_ptr(), ob, s)
+    gpu_engine.extract_device(da.data_ptr(), oa, s)
+    gpu_engine.extract_device(da.data_ptr(), oa, s)  # same key twice: descriptors not re-uploaded
+    got = [gpu_engine.hashes(c) for c in range(len(a))]
+    for c in range(len(a)):
+        assert np.array_equal(got[c], ref_a[c]), f"clip {c}"
+    # host PCM with the device batch's offsets layout, then device again
+    got_b = gpu_engine.extract_host(b)
+    for c in range(len(b)):
+        assert np.array_equal(got_b[c], ref_b[c]), f"host clip {c}"
+    gpu_engine.extract_device(db.data_ptr(), ob, s)
+    counts = gpu_engine.counts()
+    assert counts.tolist() == [len(r) for r in ref_b]
+    assert counts[1] == 0  # the 1000-sample clip has no frame
