@@ -20,8 +20,8 @@ AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
-AID_K_COUNT = 6
-KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match"]
+AID_K_COUNT = 7
+KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample"]
 
 
 class EngineUnavailable(RuntimeError):
@@ -89,11 +89,19 @@ SIGNATURES = [
     ("aid_index_finalize", ctypes.c_int, [P]),
     ("aid_index_stats", ctypes.c_int, [P, P, P, P]),
     ("aid_index_export", ctypes.c_int, [P, P, P, P, I64, I64, I32]),
+    ("aid_comm_id", ctypes.c_int, [P]),
+    ("aid_comm_create", ctypes.c_int, [P, P, I32, I32, P]),
+    ("aid_comm_destroy", None, [P]),
+    ("aid_index_allgather", ctypes.c_int, [P, P, I64, P]),
     ("aid_index_save", ctypes.c_int, [P, ctypes.c_char_p]),
     ("aid_index_load", ctypes.c_int, [P, ctypes.c_char_p]),
     ("aid_query", ctypes.c_int, [P, P, P, I32, P, P]),
     ("aid_query_extracted", ctypes.c_int, [P, P, P]),
     ("aid_downmix", ctypes.c_int, [P, P, I64, P, P]),
+    ("aid_resample_len", I64, [I64, I32, I32]),
+    ("aid_resample", ctypes.c_int, [P, P, I64, I32, I32, I32, P, I64, P, P]),
+    ("aid_resample_range", ctypes.c_int, [P, P, I64, I64, I32, I32, I32, I64, I64, P, P]),
+    ("aid_resample_plan", ctypes.c_int, [I32, I32, P, P, P, P]),
     ("aid_profile_enable", ctypes.c_int, [P, I32]),
     ("aid_profile_read", ctypes.c_int, [P, P, P, I32]),
 ]

@@ -9,10 +9,14 @@ xGMI (torch.distributed "nccl" backend = RCCL on ROCm), so every GPU holds the
 whole catalog and can answer queries alone.
 
 RCCL has no all-gatherv: counts are all-gathered first, then every rank's
-postings padded to the largest count go through a single all_gather_into_tensor
-(one [world, max_n, 3] int32 buffer), and the padding is dropped on receive.
-`allgather_postings` is device-agnostic, so the same code runs under gloo on
-CPU tensors (tests/test_catalog_dist.py) and under RCCL on GPU tensors.
+postings padded to the largest count go through a single all-gather, and the
+padding is dropped on receive. Two implementations of that exchange:
+  * "native" (default on GPUs): aid_index_allgather in libaidfp over an RCCL
+    communicator the engine owns (aid_comm_create; rank 0's unique id is shared
+    with broadcast_object_list) -- device postings never leave the C ABI;
+  * "torch": `allgather_postings` with torch.distributed collectives. It is
+    device-agnostic, so it also runs under gloo on CPU tensors
+    (tests/test_catalog_dist.py).
 """
 
 from __future__ import annotations
@@ -62,9 +66,22 @@ class IngestStats:
     t_extract: float
     t_exchange: float
     t_build: float
+    exchange: str = "none"
+    t_comm_init: float = 0.0
 
 
-def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=None) -> IngestStats:
+def native_comm(eng, group=None) -> int:
+    """aid_comm over the ranks of `group`: rank 0's RCCL id is broadcast through torch.distributed."""
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    obj = [eng.comm_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return eng.comm_create(obj[0], dist.get_world_size(group), rank)
+
+
+def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=None,
+                     exchange: str = "native") -> IngestStats:
     """Fingerprint this rank's shard of synthetic tracks on its GPU, replicate the index.
 
     `track_ids` is the full catalog (global ids); with torch.distributed initialised
@@ -91,7 +108,18 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     t1 = time.perf_counter()
     n_local = eng.index_stats()["postings"] - base
     total = n_local
-    if world > 1:
+    t_init = 0.0
+    if world > 1 and exchange == "native":
+        ti = time.perf_counter()
+        comm = native_comm(eng, group)
+        t1 = time.perf_counter()
+        t_init = t1 - ti
+        try:
+            total = eng.index_allgather(comm, base) - base
+        finally:
+            eng.comm_destroy(comm)
+        t2 = time.perf_counter()
+    elif world > 1:
         cols = torch.empty((3, max(n_local, 1)), dtype=torch.int32, device="cuda")
         eng.index_export_device(cols[0].data_ptr(), cols[1].data_ptr(), cols[2].data_ptr(), base, n_local)
         local = cols[:, :n_local].t().contiguous()
@@ -112,4 +140,5 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     eng.index_finalize()
     torch.cuda.synchronize()
     t3 = time.perf_counter()
-    return IngestStats(len(mine), len(mine) * n / eng.sample_rate, n_local, total, t1 - t0, t2 - t1, t3 - t2)
+    return IngestStats(len(mine), len(mine) * n / eng.sample_rate, n_local, total, t1 - t0 - t_init, t2 - t1,
+                       t3 - t2, exchange if world > 1 else "none", t_init)

@@ -193,6 +193,58 @@ class Engine:
         check(self._lib.aid_index_stats(self._h, ctypes.byref(n), ctypes.byref(live), ctypes.byref(nt)))
         return {"postings": n.value, "live": live.value, "tracks": nt.value}
 
+    # ---- PCM front-end (FPSPEC 8): downmix + resample, device buffers ----
+    def resample_len(self, n: int, sr_in: int, sr_out: int) -> int:
+        return int(self._lib.aid_resample_len(int(n), int(sr_in), int(sr_out)))
+
+    def resample(self, src_ptr: int, n: int, channels: int, sr_in: int, sr_out: int, dst_ptr: int, cap: int,
+                 stream: int | None = None) -> int:
+        """Asynchronous: n frames of `channels` floats at sr_in -> mono at sr_out; returns the output length."""
+        m = ctypes.c_int64(0)
+        check(self._lib.aid_resample(self._h, ctypes.c_void_p(src_ptr), int(n), int(channels), int(sr_in),
+                                     int(sr_out), ctypes.c_void_p(dst_ptr), int(cap), ctypes.byref(m),
+                                     ctypes.c_void_p(stream) if stream else None))
+        return int(m.value)
+
+    def resample_range(self, src_ptr: int, in_base: int, n: int, channels: int, sr_in: int, sr_out: int,
+                       m_first: int, count: int, dst_ptr: int, stream: int | None = None) -> None:
+        """Streaming form: stream outputs [m_first, m_first+count) from src (= stream samples
+        [in_base, in_base+n)); see include/aidfp.h."""
+        check(self._lib.aid_resample_range(self._h, ctypes.c_void_p(src_ptr), int(in_base), int(n), int(channels),
+                                           int(sr_in), int(sr_out), int(m_first), int(count),
+                                           ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream) if stream else None))
+
+    def resample_plan(self, sr_in: int, sr_out: int):
+        v = [ctypes.c_int32() for _ in range(4)]
+        if not self._lib.aid_resample_plan(int(sr_in), int(sr_out), *[ctypes.byref(x) for x in v]):
+            raise ValueError("bad sample rates")
+        return tuple(x.value for x in v)  # up, down, hl, J
+
+    # ---- native RCCL exchange (aid_comm_*, aid_index_allgather) ----
+    def comm_id(self) -> bytes:
+        """RCCL unique id (128 bytes) for aid_comm_create; made by rank 0, shared by the host."""
+        buf = (ctypes.c_uint8 * 128)()
+        check(self._lib.aid_comm_id(buf))
+        return bytes(buf)
+
+    def comm_create(self, comm_id: bytes, world: int, rank: int) -> int:
+        if len(comm_id) != 128:
+            raise ValueError("comm id must be 128 bytes")
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(comm_id)
+        check(self._lib.aid_comm_create(self._h, buf, int(world), int(rank), ctypes.byref(h)))
+        return h.value
+
+    def comm_destroy(self, comm: int) -> None:
+        if comm:
+            self._lib.aid_comm_destroy(ctypes.c_void_p(comm))
+
+    def index_allgather(self, comm: int, first: int = 0) -> int:
+        """Collective: replace postings [first, n) by the union of every rank's [first, n)."""
+        n = ctypes.c_int64(0)
+        check(self._lib.aid_index_allgather(self._h, ctypes.c_void_p(comm), int(first), ctypes.byref(n)))
+        return int(n.value)
+
     def index_export(self, first: int = 0, count: int | None = None) -> np.ndarray:
         """Host copy of stored postings [first, first+count) as [n, 3] uint32 (hash, track, t)."""
         total = self.index_stats()["postings"]

@@ -1,13 +1,18 @@
-"""Continuous identification of a 48 kHz stereo stream (BASELINE config 5).
+"""Continuous identification of a stereo stream (BASELINE config 5).
 
 The reference has no streaming path: its UI records 48 kHz mono clips
 (audio-ident-ui AudioRecorder.svelte:86-106), ffmpeg downmixes/resamples them
 (app/audio/decode.py:41-60) and each clip is one exact-lane query. Here a
-stream is consumed in chunks: every chunk of interleaved stereo is downmixed on
-the GPU (aid_downmix) into a device buffer of mono PCM, and every `hop_s` of new
-audio completes one `window_s` window (50 % overlap by default). All windows
-completed by a push are fingerprinted and matched in one batched engine call
-(K1-K3 + K5) against an index built at the stream's sample rate.
+stream is consumed in chunks, and every chunk of interleaved stereo becomes mono
+PCM at the INDEX's sample rate in a device buffer:
+  * same rate: downmix on the GPU (aid_downmix);
+  * other rate: downmix + polyphase resampling on the GPU (aid_resample_range, FPSPEC 8).
+    The raw stereo history the filter still needs stays on the device, and each push
+    produces exactly the outputs whose filter window is complete, so the chunked
+    result equals resampling the whole stream at once (tests/test_gpu_resample.py).
+Every `hop_s` of new audio completes one `window_s` window (50 % overlap by default).
+All windows completed by a push are fingerprinted and matched in one batched
+engine call (K1-K3 + K5) against the index.
 """
 
 from __future__ import annotations
@@ -28,11 +33,13 @@ class WindowResult:
 
 
 class StreamIdentifier:
-    def __init__(self, engine, window_s: float = 5.0, hop_s: float = 2.5, capacity_s: float = 120.0):
+    def __init__(self, engine, window_s: float = 5.0, hop_s: float = 2.5, capacity_s: float = 120.0,
+                 stream_sr: int | None = None):
         import torch
 
         self.eng = engine
-        self.sr = engine.sample_rate
+        self.sr = engine.sample_rate               # index rate = rate of the mono buffer
+        self.stream_sr = int(stream_sr or self.sr)
         self.win = int(round(window_s * self.sr)) & ~1
         self.hop = int(round(hop_s * self.sr)) & ~1
         cap = max(int(capacity_s * self.sr), 4 * self.win) & ~1
@@ -40,22 +47,21 @@ class StreamIdentifier:
         self.stage = torch.empty(0, dtype=torch.float32, device="cuda")
         self.win_buf = torch.empty(0, dtype=torch.float32, device="cuda")
         self.carry = np.zeros((0, 2), dtype=np.float32)  # odd trailing frame kept for the next push
-        self.filled = 0      # valid samples in self.mono (always even)
-        self.base = 0        # stream sample index of self.mono[0]
+        self.filled = 0      # valid samples in self.mono
+        self.base = 0        # stream sample index (index rate) of self.mono[0]; always even
         self.next_start = 0  # stream sample index of the next window
+        self.resampling = self.stream_sr != self.sr
+        if self.resampling:
+            self.up, self.down, self.hl, self.J = engine.resample_plan(self.stream_sr, self.sr)
+            cap_in = max(int(capacity_s * self.stream_sr), 4 * int(window_s * self.stream_sr))
+            self.raw = torch.zeros(2 * cap_in, dtype=torch.float32, device="cuda")  # interleaved stereo
+            self.raw_base = 0    # stream frame index (stream rate) of raw[0]
+            self.raw_filled = 0  # frames held
+            self.n_in = 0        # frames received
+            self.m_next = 0      # next output sample (index rate) to produce
 
-    def push(self, stereo: np.ndarray) -> list[WindowResult]:
-        """stereo: [n, 2] float32 host chunk. Returns the windows this chunk completed."""
-        import torch
-
-        x = np.ascontiguousarray(stereo, dtype=np.float32).reshape(-1, 2)
-        if len(self.carry):
-            x = np.concatenate([self.carry, x])
-        n = len(x) & ~1
-        self.carry = x[n:].copy()
-        x = x[:n]
-        if n == 0:
-            return []
+    # -- mono buffer (index rate) --
+    def _reserve_mono(self, n: int) -> None:
         if self.filled + n > self.mono.numel():  # compact: keep what pending windows still need
             drop = (self.next_start - self.base) & ~1
             keep = self.filled - drop
@@ -64,12 +70,65 @@ class StreamIdentifier:
             self.mono[:keep] = self.mono[drop:self.filled].clone()
             self.base += drop
             self.filled = keep
+
+    def _push_same_rate(self, x: np.ndarray, s: int) -> None:
+        import torch
+
+        if len(self.carry):
+            x = np.concatenate([self.carry, x])
+        n = len(x) & ~1
+        self.carry = x[n:].copy()
+        x = x[:n]
+        if n == 0:
+            return
+        self._reserve_mono(n)
         if self.stage.numel() < 2 * n:
             self.stage = torch.empty(2 * n, dtype=torch.float32, device="cuda")
         self.stage[: 2 * n].copy_(torch.from_numpy(x.reshape(-1)))
-        s = torch.cuda.current_stream().cuda_stream
         self.eng.downmix(self.stage.data_ptr(), n, self.mono.data_ptr() + 4 * self.filled, s)
         self.filled += n
+
+    def _push_resampled(self, x: np.ndarray, s: int) -> None:
+        import torch
+
+        n = len(x)
+        if n == 0:
+            return
+        cap_in = self.raw.numel() // 2
+        if self.raw_filled + n > cap_in:  # compact: keep the input the next output still reads
+            need = max(self.raw_base, (self.m_next * self.down + self.hl) // self.up - (self.J - 1))
+            drop = need - self.raw_base
+            keep = self.raw_filled - drop
+            if keep + n > cap_in:
+                raise ValueError("chunk larger than the stream buffer")
+            self.raw[: 2 * keep] = self.raw[2 * drop: 2 * self.raw_filled].clone()
+            self.raw_base += drop
+            self.raw_filled = keep
+        self.raw[2 * self.raw_filled: 2 * (self.raw_filled + n)].copy_(torch.from_numpy(x.reshape(-1)))
+        self.raw_filled += n
+        self.n_in += n
+        # outputs m whose last input floor((m*down + hl)/up) has arrived
+        last = self.n_in * self.up - 1 - self.hl
+        m_ready = last // self.down + 1 if last >= 0 else 0
+        count = m_ready - self.m_next
+        if count <= 0:
+            return
+        self._reserve_mono(count)
+        self.eng.resample_range(self.raw.data_ptr(), self.raw_base, self.raw_filled, 2, self.stream_sr, self.sr,
+                                self.m_next, count, self.mono.data_ptr() + 4 * self.filled, s)
+        self.filled += count
+        self.m_next = m_ready
+
+    def push(self, stereo: np.ndarray) -> list[WindowResult]:
+        """stereo: [n, 2] float32 host chunk at stream_sr. Returns the windows this chunk completed."""
+        import torch
+
+        x = np.ascontiguousarray(stereo, dtype=np.float32).reshape(-1, 2)
+        s = torch.cuda.current_stream().cuda_stream
+        if self.resampling:
+            self._push_resampled(x, s)
+        else:
+            self._push_same_rate(x, s)
         starts = []
         while self.next_start + self.win <= self.base + self.filled:
             starts.append(self.next_start)
@@ -86,3 +145,7 @@ class StreamIdentifier:
         self.eng.extract_device(self.win_buf.data_ptr(), np.arange(k + 1, dtype=np.int64) * self.win, s)
         rows = self.eng.query_extracted()
         return [WindowResult(st / self.sr, r) for st, r in zip(starts, rows)]
+
+    def mono_history(self) -> np.ndarray:
+        """Host copy of the mono buffer (index rate) currently held, from stream sample self.base."""
+        return self.mono[: self.filled].cpu().numpy()

@@ -20,7 +20,8 @@ LIB = PKG / "aidfp" / "libaidfp.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "stream.hip", "engine.cpp"]
+SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "stream.hip", "resample.hip",
+           "engine.cpp"]
 FLAGS = [
     f"--offload-arch={ARCH}",
     "-O3",
@@ -63,7 +64,9 @@ def build(verbose: bool = False, variant: str | None = None, defines: tuple = ()
         objs = list(ex.map(lambda s: _compile(s, verbose, objdir, extra), srcs))
     if lib.exists() and all(o.stat().st_mtime <= lib.stat().st_mtime for o in objs):
         return lib
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs)]
+    # librccl.so.1: the same SONAME torch bundles, so one RCCL runtime per process (like the HIP one)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib), *map(str, objs),
+           "-L/opt/rocm/lib", "-lrccl"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -14,9 +14,15 @@ constexpr int kFan = 10;          // targets per anchor
 constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 
 // K1: 12 waves per workgroup, each wave slides over a strip of kStftStrip frames
-constexpr int kStftWaves = 12;
+#ifndef AID_STFT_WAVES
+#define AID_STFT_WAVES 12
+#endif
+constexpr int kStftWaves = AID_STFT_WAVES;
 constexpr int kStftStrip = 16;
-constexpr int kStftLdsPerWave = 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024+32)
+#ifndef AID_K1_COMPACT
+#define AID_K1_COMPACT 0
+#endif
+constexpr int kStftLdsPerWave = AID_K1_COMPACT ? 1024 : 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024)
 
 // K2: output frames per workgroup strip
 constexpr int kPeakStrip = 128;

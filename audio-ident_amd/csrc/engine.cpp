@@ -5,11 +5,13 @@
 // results. Replaces the `olaf_c` process boundary of the reference
 // (audio-ident-service/app/audio/fingerprint.py:87-270).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -17,6 +19,7 @@
 #include "../../include/aidfp.h"
 #include "aidfp_device.h"
 #include "aidfp_layout.h"
+#include "resample_design.h"
 
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_strips, int hop,
@@ -27,6 +30,9 @@ void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, 
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
                   int noise_a, uint32_t salt, const int16_t *sin_tab, hipStream_t s);
+int64_t resample_lds_floats(int up, int down, int J);
+void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
+                     const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s);
 void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
                         uint32_t *cnt, hipStream_t s);
 void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
@@ -132,6 +138,9 @@ struct aid_engine {
     DevBuf<uint32_t> q_hist;
     DevBuf<int32_t> q_rows, q_nrows;
     DevBuf<int64_t> x_src, x_dst;
+    DevBuf<int64_t> g_meta;            // all-gather: (count, n_tracks) per rank
+    std::map<std::pair<int32_t, int32_t>, float *> rs_taps;  // (up, down) -> device [up][J] taps
+    DevBuf<uint32_t> g_send, g_recv;   // all-gather: [3][max] SoA planes per rank
     DevBuf<uint32_t> x_tracks;
     size_t hist_zero_cap = 0;  // q_hist capacity known to be all-zero
 
@@ -308,6 +317,10 @@ void aid_engine_destroy(aid_engine *e) {
     e->q_nrows.release();
     e->x_src.release();
     e->x_dst.release();
+    e->g_meta.release();
+    for (auto &kv : e->rs_taps) (void)hipFree(kv.second);
+    e->g_send.release();
+    e->g_recv.release();
     e->x_tracks.release();
     if (e->h_desc) (void)hipHostFree(e->h_desc);
     if (e->desc_ev) (void)hipEventDestroy(e->desc_ev);
@@ -583,6 +596,85 @@ int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *
     return AID_OK;
 }
 
+int aid_resample_plan(int32_t sr_in, int32_t sr_out, int32_t *up, int32_t *down, int32_t *hl, int32_t *J) {
+    ResamplePlan p;
+    if (!resample_plan(sr_in, sr_out, p)) return 0;
+    if (up) *up = p.up;
+    if (down) *down = p.down;
+    if (hl) *hl = p.hl;
+    if (J) *J = p.J;
+    return 1;
+}
+
+int64_t aid_resample_len(int64_t n, int32_t sr_in, int32_t sr_out) {
+    ResamplePlan p;
+    if (n <= 0 || !resample_plan(sr_in, sr_out, p)) return 0;
+    return (n * p.up + p.down - 1) / p.down;
+}
+
+static int resample_taps_dev(aid_engine *e, const ResamplePlan &p, float **out) {
+    auto it = e->rs_taps.find({p.up, p.down});
+    if (it != e->rs_taps.end()) {
+        *out = it->second;
+        return AID_OK;
+    }
+    const std::vector<float> h = resample_phase_taps(p);
+    float *taps = nullptr;
+    HIP_TRY(hipMalloc(&taps, h.size() * sizeof(float)));
+    hipError_t he = hipMemcpy(taps, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (he != hipSuccess) {
+        (void)hipFree(taps);
+        return fail(AID_ERR_DEVICE, std::string("aid_resample: ") + hipGetErrorString(he));
+    }
+    e->rs_taps[{p.up, p.down}] = taps;
+    *out = taps;
+    return AID_OK;
+}
+
+int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t n, int32_t channels, int32_t sr_in,
+                       int32_t sr_out, int64_t m_first, int64_t count, float *dst, void *stream) {
+    if (!e || n < 0 || in_base < 0 || m_first < 0 || count < 0 || (channels != 1 && channels != 2))
+        return fail(AID_ERR_INVALID, "aid_resample: bad argument");
+    ResamplePlan p;
+    if (!resample_plan(sr_in, sr_out, p)) return fail(AID_ERR_INVALID, "aid_resample: sample rates must be > 0");
+    if (count == 0) return AID_OK;
+    if (!dst || (n > 0 && !src)) return fail(AID_ERR_INVALID, "aid_resample: null buffer");
+    if (channels == 2 && (reinterpret_cast<uintptr_t>(src) & 7))
+        return fail(AID_ERR_INVALID, "aid_resample: stereo src must be 8-byte aligned");
+    if (resample_lds_floats(p.up, p.down, p.J) * 4 > 65536)
+        return fail(AID_ERR_INVALID, "aid_resample: down/up ratio too large (LDS window > 64 KB)");
+    if ((int64_t)p.up * p.J > (1 << 24)) return fail(AID_ERR_INVALID, "aid_resample: tap table too large");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = pick_stream(e, stream);
+    float *taps = nullptr;
+    if (int rc = resample_taps_dev(e, p, &taps)) return rc;
+    {
+        ProfScope ps(e, AID_K_RESAMPLE, s);
+        launch_resample(src, in_base, n, channels, p.up, p.down, p.hl, p.J, taps, dst, m_first, count, s);
+    }
+    HIP_TRY(hipGetLastError());
+    return AID_OK;
+}
+
+int aid_resample(aid_engine *e, const float *src, int64_t n, int32_t channels, int32_t sr_in, int32_t sr_out,
+                 float *dst, int64_t cap, int64_t *n_out, void *stream) {
+    if (!e || n < 0 || (channels != 1 && channels != 2)) return fail(AID_ERR_INVALID, "aid_resample: bad argument");
+    const int64_t m = aid_resample_len(n, sr_in, sr_out);
+    if (n > 0 && m == 0) return fail(AID_ERR_INVALID, "aid_resample: sample rates must be > 0");
+    if (n_out) *n_out = m;
+    if (m > cap) return fail(AID_ERR_INVALID, "aid_resample: output capacity too small");
+    if (m == 0) return AID_OK;
+    if (sr_in == sr_out && channels == 1) {  // same rate, mono: a copy
+        if (!src || !dst) return fail(AID_ERR_INVALID, "aid_resample: null buffer");
+        std::lock_guard<std::mutex> lk(e->mu);
+        HIP_TRY(hipSetDevice(e->device));
+        HIP_TRY(hipMemcpyAsync(dst, src, n * sizeof(float), hipMemcpyDeviceToDevice, pick_stream(e, stream)));
+        return AID_OK;
+    }
+    return aid_resample_range(e, src, 0, n, channels, sr_in, sr_out, 0, m, dst, stream);
+}
+
 int aid_profile_enable(aid_engine *e, int32_t on) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     e->profiling = on != 0;
@@ -782,6 +874,111 @@ int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_
     if (n_postings) *n_postings = e->n_post;
     if (n_live) *n_live = e->index_built && !e->index_dirty ? e->n_indexed : -1;
     if (n_tracks) *n_tracks = e->n_tracks;
+    return AID_OK;
+}
+
+}  // extern "C"
+
+struct aid_comm {
+    ncclComm_t comm = nullptr;
+    int world = 0, rank = 0, device = -1;
+};
+
+#define NCCL_TRY(expr)                                                                              \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess) return fail(AID_ERR_DEVICE, std::string(#expr ": ") + ncclGetErrorString(r_)); \
+    } while (0)
+
+extern "C" {
+
+int aid_comm_id(uint8_t id[AID_COMM_ID_BYTES]) {
+    if (!id) return fail(AID_ERR_INVALID, "null id");
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    static_assert(sizeof(u.internal) == AID_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(id, u.internal, AID_COMM_ID_BYTES);
+    return AID_OK;
+}
+
+int aid_comm_create(aid_engine *e, const uint8_t id[AID_COMM_ID_BYTES], int32_t world, int32_t rank, aid_comm **out) {
+    if (!e || !id || !out || world <= 0 || rank < 0 || rank >= world) return fail(AID_ERR_INVALID, "aid_comm_create: bad argument");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(e->device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, AID_COMM_ID_BYTES);
+    ncclComm_t c = nullptr;
+    NCCL_TRY(ncclCommInitRank(&c, world, u, rank));
+    aid_comm *ac = new aid_comm();
+    ac->comm = c;
+    ac->world = world;
+    ac->rank = rank;
+    ac->device = e->device;
+    *out = ac;
+    return AID_OK;
+}
+
+void aid_comm_destroy(aid_comm *c) {
+    if (!c) return;
+    if (c->comm) {
+        (void)hipSetDevice(c->device);
+        (void)ncclCommDestroy(c->comm);
+    }
+    delete c;
+}
+
+int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_total) {
+    if (!e || !c || !c->comm) return fail(AID_ERR_INVALID, "aid_index_allgather: null argument");
+    if (c->device != e->device) return fail(AID_ERR_INVALID, "aid_index_allgather: comm and engine on different devices");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "aid_index_allgather: first out of range");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    const int W = c->world;
+    const int64_t n_local = e->n_post - first;
+    // 1. (count, n_tracks) of every rank: sizes the padded exchange and the track tables
+    HIP_TRY(e->g_meta.reserve(2 * (size_t)W + 2));
+    const int64_t mine[2] = {n_local, (int64_t)e->n_tracks};
+    HIP_TRY(hipMemcpyAsync(e->g_meta.p, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+    NCCL_TRY(ncclAllGather(e->g_meta.p, e->g_meta.p + 2, 2, ncclInt64, c->comm, s));
+    std::vector<int64_t> meta(2 * (size_t)W);
+    HIP_TRY(hipMemcpyAsync(meta.data(), e->g_meta.p + 2, meta.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    int64_t mx = 0, tot = 0, tracks = 0;
+    for (int r = 0; r < W; ++r) {
+        mx = std::max(mx, meta[2 * r]);
+        tot += meta[2 * r];
+        tracks = std::max(tracks, meta[2 * r + 1]);
+    }
+    if (first + tot > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "aid_index_allgather: more than 2^32 postings");
+    if (mx > 0) {
+        // 2. own shard as [3][mx] planes (the tail past n_local is padding), one all-gather
+        HIP_TRY(e->g_send.reserve(3 * (size_t)mx));
+        HIP_TRY(e->g_recv.reserve(3 * (size_t)mx * W));
+        uint32_t *planes[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
+        for (int q = 0; q < 3 && n_local > 0; ++q)
+            HIP_TRY(hipMemcpyAsync(e->g_send.p + q * mx, planes[q] + first, n_local * sizeof(uint32_t),
+                                   hipMemcpyDeviceToDevice, s));
+        NCCL_TRY(ncclAllGather(e->g_send.p, e->g_recv.p, 3 * (size_t)mx, ncclUint32, c->comm, s));
+        // 3. the union in rank order replaces this rank's shard
+        e->n_post = first;
+        if (int rc = reserve_postings(e, tot, s)) return rc;
+        if (int rc = ensure_tracks(e, (uint32_t)tracks, s)) return rc;
+        uint32_t *dst[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
+        int64_t at = first;
+        for (int r = 0; r < W; ++r) {
+            const int64_t n = meta[2 * r];
+            for (int q = 0; q < 3 && n > 0; ++q)
+                HIP_TRY(hipMemcpyAsync(dst[q] + at, e->g_recv.p + ((size_t)r * 3 + q) * mx, n * sizeof(uint32_t),
+                                       hipMemcpyDeviceToDevice, s));
+            at += n;
+        }
+        HIP_TRY(hipStreamSynchronize(s));
+        e->n_post = at;
+        e->index_dirty = true;
+    }
+    if (n_total) *n_total = e->n_post;
     return AID_OK;
 }
 

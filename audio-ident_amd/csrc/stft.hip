@@ -34,6 +34,8 @@
 #ifndef AID_K1_DIAG
 #define AID_K1_DIAG 0
 #endif
+// AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
+// (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
 
 namespace aid {
 
@@ -50,17 +52,26 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                                                 float *__restrict__ out) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
-    __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68, E2: 64 x 17, E3: 1024
+    __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
     // tables as float4 pairs [h][lane], one ds_read_b128 per pair (hipcc would otherwise merge the
     // stride-512-B float2 reads into ds_read2st64_b64, which costs the LDS twice the cycles):
     //   s_win4[h] = window of rows 2h, 2h+1 ; s_ta4[h] = T1K[lane*k1], k1 = 2h, 2h+1
     //   s_tb4[h] = T64[(lane&3)*j1], j1 = 2h, 2h+1 ; s_t2p[i] = (T2K[k], T2K[1024-k]), k = lane + 64i
-    __shared__ float4 s_win4[512], s_ta4[512], s_tb4[512], s_t2p[512];
+    __shared__ float4 s_win4[512], s_ta4[512], s_t2p[512];
+    __shared__ float4 s_tb4[32];  // [h][lane & 3]: T64[m2*j1] depends on the lane only through m2
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     float2 *buf = lds[wave];
     const int kq = lane >> 2;  // stage B/C: k1
     const int mq = lane & 3;   // stage B: m2 ; stage C: s
+    // E3 addresses as one per-lane base + compile-time offsets (the XOR only touches bits 2-3):
+    //   stage-C slot of Z[kq + 16(mq+4r) + 256 j2]: bits 4-5 of k are mq      -> e3w + 64r + 256 j2
+    //   Z[lane + 64i]: bits 4-5 are those of lane                              -> e3a + 64i
+    //   Z[1024 - lane - 64i] = Z[64(15-i) + m], m = 64 - lane in 1..64         -> e3b + 64(15-i)
+    //   (except k = 0, whose mirror is Z[0] itself)
+    const int e3w = (kq ^ (mq << 2)) + 16 * mq;
+    const int e3a = e3(lane);
+    const int e3b = e3(64 - lane);
 
     for (int i = threadIdx.x; i < 512; i += kStftWaves * 64) {
         const int h = i >> 6, l = i & 63, a = 2 * h, b = 2 * h + 1;
@@ -68,8 +79,10 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
         s_win4[i] = make_float4(w0.x, w0.y, w1.x, w1.y);
         const float2 ta0 = tab->t1k[l * a], ta1 = tab->t1k[l * b];
         s_ta4[i] = make_float4(ta0.x, ta0.y, ta1.x, ta1.y);
-        const float2 tb0 = tab->t64[(l & 3) * a], tb1 = tab->t64[(l & 3) * b];
-        s_tb4[i] = make_float4(tb0.x, tb0.y, tb1.x, tb1.y);
+        if (l < 4) {
+            const float2 tb0 = tab->t64[l * a], tb1 = tab->t64[l * b];
+            s_tb4[4 * h + l] = make_float4(tb0.x, tb0.y, tb1.x, tb1.y);
+        }
         const int k = l + 64 * h;
         const float2 c0 = tab->t2k[k], c1 = tab->t2k[(1024 - k) & 1023];  // k = 0: mirror unused
         s_t2p[i] = make_float4(c0.x, c0.y, c1.x, c1.y);
@@ -127,30 +140,37 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
                 if (AID_K1_DIAG != 6) {
 #pragma unroll
-                    for (int k1 = 0; k1 < 16; ++k1) buf[k1 * 68 + lane] = v[k1];
+                    for (int k1 = 0; k1 < 16; ++k1)
+                        buf[AID_K1_COMPACT ? k1 * 64 + (lane ^ (4 * (k1 & 7))) : k1 * 68 + lane] = v[k1];
                     wave_lds_sync();
 #pragma unroll
-                    for (int m1 = 0; m1 < 16; ++m1) v[m1] = buf[AID_K1_DIAG == 4 ? m1 * 68 + lane : kq * 68 + 4 * m1 + mq];
+                    for (int m1 = 0; m1 < 16; ++m1)
+                        v[m1] = buf[AID_K1_DIAG == 4    ? m1 * 68 + lane
+                                    : AID_K1_COMPACT ? kq * 64 + 4 * ((m1 & 8) | ((m1 ^ kq) & 7)) + mq
+                                                     : kq * 68 + 4 * m1 + mq];
                     wave_lds_sync();
                 }
                 // stage B
                 if (AID_K1_DIAG != 9) dft16(v, t16);
 #pragma unroll
                 for (int h = 0; h < 8; ++h) {
-                    const float4 t = s_tb4[64 * h + lane];
+                    const float4 t = s_tb4[4 * h + mq];
                     if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
                     v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
                 }
                 // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
                 if (AID_K1_DIAG != 7) {
 #pragma unroll
-                    for (int j1 = 0; j1 < 16; ++j1) buf[lane * 17 + j1] = v[j1];
+                    for (int j1 = 0; j1 < 16; ++j1)
+                        buf[AID_K1_COMPACT ? j1 * 64 + (lane ^ (j1 & 3)) : lane * 17 + j1] = v[j1];
                     wave_lds_sync();
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
                         for (int m2 = 0; m2 < 4; ++m2)
-                            v[4 * r + m2] = buf[AID_K1_DIAG == 5 ? (4 * r + m2) * 68 + lane : (4 * kq + m2) * 17 + mq + 4 * r];
+                            v[4 * r + m2] = buf[AID_K1_DIAG == 5    ? (4 * r + m2) * 68 + lane
+                                                : AID_K1_COMPACT ? (mq + 4 * r) * 64 + 4 * kq + (m2 ^ mq)
+                                                                 : (4 * kq + m2) * 17 + mq + 4 * r];
                     wave_lds_sync();
                 }
                 // stage C: DFT4 over m2 -> Z[kq + 16*(mq + 4r) + 256*j2]; E3 natural order, pad 1 per 32
@@ -159,8 +179,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     dft4(v[4 * r + 0], v[4 * r + 1], v[4 * r + 2], v[4 * r + 3]);
 #pragma unroll
                     for (int j2 = 0; j2 < 4; ++j2) {
-                        const int k = AID_K1_DIAG == 1 ? lane + 64 * (r + 4 * j2) : kq + 16 * (mq + 4 * r) + 256 * j2;
-                        if (AID_K1_DIAG != 8) buf[e3(k)] = v[4 * r + j2];
+                        const int a = AID_K1_DIAG == 1 ? lane + 64 * (r + 4 * j2) : e3w + 64 * r + 256 * j2;
+                        if (AID_K1_DIAG != 8) buf[a] = v[4 * r + j2];
                     }
                 }
                 wave_lds_sync();
@@ -172,9 +192,10 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const int k = lane + 64 * i;  // 0..511
-                    const int kk = (1024 - k) & 1023;
-                    const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[e3(k)];
-                    const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[e3(AID_K1_DIAG == 2 ? (k ^ 512) : kk)];
+                    const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[e3a + 64 * i];
+                    // k = 0 mirrors onto itself (Z[0]): lane 0's e3b + 960 would be slot 1024
+                    const int bi = (i == 0 && lane == 0) ? 0 : e3b + 64 * (15 - i);
+                    const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[AID_K1_DIAG == 2 ? e3(k ^ 512) : bi];
                     const float er = a.x + b.x, ei = a.y - b.y;
                     const float orr = a.y + b.y, oi = b.x - a.x;
                     const float4 t2 = s_t2p[64 * i + lane];

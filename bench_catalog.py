@@ -33,6 +33,8 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--sr", type=int, default=44100)
     ap.add_argument("--check", type=int, default=64, help="spot-check queries on rank 0")
+    ap.add_argument("--exchange", choices=("native", "torch"), default="native",
+                    help="native: aid_index_allgather over the engine's RCCL comm; torch: torch.distributed")
     args = ap.parse_args()
 
     import torch
@@ -55,15 +57,16 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = ingest_synthetic(eng, tracks, args.seconds, batch=args.batch)
+    st = ingest_synthetic(eng, tracks, args.seconds, batch=args.batch, exchange=args.exchange)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    phases = torch.tensor([wall, st.t_extract, st.t_exchange, st.t_build], dtype=torch.float64, device="cuda")
+    phases = torch.tensor([wall, st.t_extract, st.t_exchange, st.t_build, st.t_comm_init], dtype=torch.float64,
+                          device="cuda")
     if world > 1:
         dist.all_reduce(phases, op=dist.ReduceOp.MAX)
-    wall, te, tx, tb = phases.tolist()
+    wall, te, tx, tb, ti = phases.tolist()
 
     acc = None
     if rank == 0 and args.check:
@@ -81,7 +84,9 @@ def main() -> int:
             "metric": "catalog ingest audio-seconds/sec (extract + RCCL all-gather + index build), whole job",
             "value": round(audio / wall, 1), "unit": "audio-s/s", "n_gpus": world, "tracks": args.tracks,
             "track_seconds": args.seconds, "wall_s": round(wall, 3),
-            "phase_s_max_over_ranks": {"extract": round(te, 3), "allgather": round(tx, 3), "build": round(tb, 3)},
+            "phase_s_max_over_ranks": {"extract": round(te, 3), "allgather": round(tx, 3), "build": round(tb, 3),
+                                       "comm_init": round(ti, 3)},
+            "exchange": st.exchange,
             "postings_total": st.postings_total, "index_bytes_per_gpu": st.postings_total * 8 + (2**26 + 1) * 4,
             "top1_spot_check": acc, "data": "synthetic (aid_synth, generated in HBM)",
         }), flush=True)

@@ -43,7 +43,8 @@ extern "C" {
 #define AID_K_LANDMARK_WRITE 3
 #define AID_K_SYNTH 4
 #define AID_K_MATCH 5
-#define AID_K_COUNT 6
+#define AID_K_RESAMPLE 6
+#define AID_K_COUNT 7
 
 typedef struct aid_engine aid_engine;
 
@@ -144,6 +145,41 @@ int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_
 /* Copy stored postings [first, first+count) to host or device columns (RCCL all-gather export). */
 int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t, int64_t first, int64_t count,
                      int32_t location);
+/* ---- PCM front-end (spec/FPSPEC.md 8) ----
+ * Replaces ffmpeg `-ac 1 -ar <rate>` (audio-ident-service/app/audio/decode.py:41-60): optional
+ * stereo downmix ((L+R)*0.5f) + rational polyphase resampling sr_in -> sr_out (scipy
+ * resample_poly's Kaiser(5) filter, binary32, pinned order). src/dst are device pointers; src
+ * holds n frames of `channels` (1, or 2 interleaved) floats, dst receives
+ * aid_resample_len(n, sr_in, sr_out) mono samples. Asynchronous on `stream` (NULL = engine). */
+int64_t aid_resample_len(int64_t n, int32_t sr_in, int32_t sr_out);
+int aid_resample(aid_engine *e, const float *src, int64_t n, int32_t channels, int32_t sr_in, int32_t sr_out,
+                 float *dst, int64_t cap, int64_t *n_out, void *stream);
+/* Streaming form: src[0] is stream sample in_base (samples outside [in_base, in_base+n) read as 0);
+ * computes stream outputs [m_first, m_first+count) into dst[0..count). Output m needs inputs up to
+ * floor((m*down + hl)/up) and J-1 before it, so a caller that keeps that history gets exactly the
+ * whole-signal result chunk by chunk (aidfp.stream). */
+int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t n, int32_t channels, int32_t sr_in,
+                       int32_t sr_out, int64_t m_first, int64_t count, float *dst, void *stream);
+/* (up, down, hl, J) of a rate pair (FPSPEC 8); returns 0 on bad rates */
+int aid_resample_plan(int32_t sr_in, int32_t sr_out, int32_t *up, int32_t *down, int32_t *hl, int32_t *J);
+
+/* ---- native multi-GPU exchange (SURVEY.md 8b "aid_allgather_index", 8e) ----
+ * One process per GPU. Rank 0 calls aid_comm_id, the host hands the 128 id bytes to every
+ * rank (any side channel: torch.distributed store, MPI, a file), then every rank calls
+ * aid_comm_create with its own engine. aid_comm wraps an RCCL communicator over xGMI.
+ * Replaces the reference's single LMDB writer (pipeline.py:294-310, fingerprint.py:7-8):
+ * ingest is sharded, the index is replicated by ONE all-gather. */
+#define AID_COMM_ID_BYTES 128
+typedef struct aid_comm aid_comm;
+int aid_comm_id(uint8_t id[AID_COMM_ID_BYTES]);
+int aid_comm_create(aid_engine *e, const uint8_t id[AID_COMM_ID_BYTES], int32_t world, int32_t rank, aid_comm **out);
+void aid_comm_destroy(aid_comm *c);
+/* Collective over all ranks of c: every rank's postings [first, n) (its shard) are all-gathered
+ * (counts and track-id ranges first, then one padded SoA all-gather) and replace [first, n) by
+ * the union in rank order; postings before `first` stay. The index is left dirty (finalize
+ * next). *n_total = postings now held. Every rank must call it with the same comm. */
+int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_total);
+
 /* Flat versioned file (magic AIDFPIX1 + header + posting columns + tombstones): replaces the OLAF_DB dir. */
 int aid_index_save(aid_engine *e, const char *path);
 int aid_index_load(aid_engine *e, const char *path);

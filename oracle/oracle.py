@@ -34,7 +34,7 @@ DEFAULT_THR = 4.0
 
 
 def build() -> Path:
-    srcs = [HERE / "fp_oracle.c", HERE / "fp_match.c"]
+    srcs = [HERE / "fp_oracle.c", HERE / "fp_match.c", HERE / "fp_resample.c"]
     if not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
@@ -85,6 +85,12 @@ def lib():
         L.fp_index_sort.argtypes = [P, i64]
         L.fp_query.restype = i64
         L.fp_query.argtypes = [P, i64, P, P, i64, ctypes.c_int32, P, i64]
+        L.fp_resample_ratio.argtypes = [ctypes.c_int32] * 2 + [P] * 4
+        L.fp_resample_taps.argtypes = [ctypes.c_int32, ctypes.c_int32, P]
+        L.fp_resample_len.restype = i64
+        L.fp_resample_len.argtypes = [i64, ctypes.c_int32, ctypes.c_int32]
+        L.fp_resample.restype = i64
+        L.fp_resample.argtypes = [P, i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P]
         _lib = L
     return _lib
 
@@ -205,3 +211,28 @@ if os.environ.get("AIDFP_ORACLE_AUTOBUILD", "1") == "1" and not LIB_PATH.exists(
         build()
     except Exception:  # pragma: no cover - surfaced by lib()
         pass
+
+
+# ---- PCM front-end (FPSPEC 8): downmix + rational resampling ----
+def resample_ratio(sr_in: int, sr_out: int):
+    v = [ctypes.c_int32() for _ in range(4)]
+    if not lib().fp_resample_ratio(sr_in, sr_out, *[ctypes.byref(x) for x in v]):
+        raise ValueError("bad sample rates")
+    return tuple(x.value for x in v)  # up, down, hl, J
+
+
+def resample_taps(sr_in: int, sr_out: int) -> np.ndarray:
+    up, down, hl, _ = resample_ratio(sr_in, sr_out)
+    t = np.zeros(2 * hl + 1, np.float32)
+    lib().fp_resample_taps(up, down, _ptr(t))
+    return t
+
+
+def resample(x: np.ndarray, sr_in: int, sr_out: int) -> np.ndarray:
+    """x: [n] mono or [n, 2] interleaved stereo float32 -> mono float32 at sr_out."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    ch = 1 if x.ndim == 1 else x.shape[1]
+    n = x.shape[0]
+    y = np.zeros(max(1, int(lib().fp_resample_len(n, sr_in, sr_out))), np.float32)
+    m = lib().fp_resample(_ptr(x), n, ch, sr_in, sr_out, _ptr(y))
+    return y[:m]

@@ -37,3 +37,23 @@ def test_abi_version_and_defaults_without_gpu():
     assert L.aid_config_default(16000, ctypes.byref(cfg)) == 0 and cfg.hop == 256
     assert L.aid_config_default(0, ctypes.byref(cfg)) == _lib.AID_ERR_INVALID
     assert "bad argument" in _lib.last_error()
+
+
+def test_python_constants_match_header():
+    """Every #define AID_* the Python side mirrors has the header's value (a stale
+    AID_K_COUNT would make aid_profile_read write past the ctypes arrays)."""
+    defs = dict(re.findall(r"#define\s+(AID_[A-Z0-9_]+)\s+(-?\d+)", HEADER.read_text()))
+    mirrored = {k: getattr(_lib, k) for k in defs if hasattr(_lib, k)}
+    assert "AID_K_COUNT" in mirrored and len(mirrored) >= 5
+    for k, v in mirrored.items():
+        assert v == int(defs[k]), k
+    assert len(_lib.KERNEL_NAMES) == int(defs["AID_K_COUNT"])
+
+
+def test_resample_len_without_gpu():
+    L = _lib.load()
+    assert L.aid_resample_len(48000, 48000, 16000) == 16000
+    assert L.aid_resample_len(48001, 48000, 16000) == 16001
+    assert L.aid_resample_len(1000, 44100, 48000) == 1089  # ceil(1000 * 160 / 147)
+    assert L.aid_resample_len(0, 48000, 16000) == 0
+    assert L.aid_resample_len(10, 0, 16000) == 0
