@@ -20,8 +20,9 @@ AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
-AID_K_COUNT = 7
-KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample"]
+AID_K_COUNT = 8
+KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample",
+                "dedup"]
 
 
 class EngineUnavailable(RuntimeError):
@@ -102,6 +103,11 @@ SIGNATURES = [
     ("aid_resample", ctypes.c_int, [P, P, I64, I32, I32, I32, P, I64, P, P]),
     ("aid_resample_range", ctypes.c_int, [P, P, I64, I64, I32, I32, I32, I64, I64, P, P]),
     ("aid_resample_plan", ctypes.c_int, [I32, I32, P, P, P, P]),
+    ("aid_dedup_reset", ctypes.c_int, [P]),
+    ("aid_dedup_add", ctypes.c_int, [P, P, P, P, I32]),
+    ("aid_dedup_count", ctypes.c_int, [P, P, P]),
+    ("aid_dedup_scan", ctypes.c_int, [P, P, P, P, I32, P, P]),
+    ("aid_dedup_pairs", ctypes.c_int, [P, P, P, P, P, I32, P]),
     ("aid_profile_enable", ctypes.c_int, [P, I32]),
     ("aid_profile_read", ctypes.c_int, [P, P, P, I32]),
 ]

@@ -33,6 +33,12 @@ void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int
 int64_t resample_lds_floats(int up, int down, int J);
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
                      const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s);
+int dedup_chunks(int64_t n_cat);
+void launch_dedup_scan(const uint32_t *cw, const int64_t *coff, const double *cdur, int64_t n_cat, const uint32_t *qw,
+                       const int64_t *qoff, const double *qlo, const double *qhi, int nq, double *part_sim,
+                       int64_t *part_idx, double *best_sim, int64_t *best_idx, hipStream_t s);
+void launch_dedup_pairs(const uint32_t *aw, const int64_t *aoff, const uint32_t *bw, const int64_t *boff, int n,
+                        double *sim, hipStream_t s);
 void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
                         uint32_t *cnt, hipStream_t s);
 void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
@@ -140,6 +146,14 @@ struct aid_engine {
     DevBuf<int64_t> x_src, x_dst;
     DevBuf<int64_t> g_meta;            // all-gather: (count, n_tracks) per rank
     std::map<std::pair<int32_t, int32_t>, float *> rs_taps;  // (up, down) -> device [up][J] taps
+    // Chromaprint dedup catalog (insertion order) + scan scratch
+    DevBuf<uint32_t> dd_words;
+    DevBuf<int64_t> dd_off;
+    DevBuf<double> dd_dur;
+    int64_t dd_n = 0, dd_nw = 0;
+    DevBuf<uint32_t> dq_words, dq_words2;
+    DevBuf<int64_t> dq_off, dq_off2, dq_idx, dq_pidx;
+    DevBuf<double> dq_lo, dq_hi, dq_sim, dq_psim;
     DevBuf<uint32_t> g_send, g_recv;   // all-gather: [3][max] SoA planes per rank
     DevBuf<uint32_t> x_tracks;
     size_t hist_zero_cap = 0;  // q_hist capacity known to be all-zero
@@ -319,6 +333,19 @@ void aid_engine_destroy(aid_engine *e) {
     e->x_dst.release();
     e->g_meta.release();
     for (auto &kv : e->rs_taps) (void)hipFree(kv.second);
+    e->dd_words.release();
+    e->dd_off.release();
+    e->dd_dur.release();
+    e->dq_words.release();
+    e->dq_words2.release();
+    e->dq_off.release();
+    e->dq_off2.release();
+    e->dq_idx.release();
+    e->dq_pidx.release();
+    e->dq_lo.release();
+    e->dq_hi.release();
+    e->dq_sim.release();
+    e->dq_psim.release();
     e->g_send.release();
     e->g_recv.release();
     e->x_tracks.release();
@@ -673,6 +700,141 @@ int aid_resample(aid_engine *e, const float *src, int64_t n, int32_t channels, i
         return AID_OK;
     }
     return aid_resample_range(e, src, 0, n, channels, sr_in, sr_out, 0, m, dst, stream);
+}
+
+}  // extern "C"
+
+// grow a device buffer to hold `want` elements, keeping the first `keep` (stream-ordered copy)
+template <typename T>
+static int grow_keep(DevBuf<T> &b, size_t keep, size_t want, hipStream_t s) {
+    if (want <= b.n) return AID_OK;
+    size_t cap = std::max(want, b.n * 2);
+    T *p = nullptr;
+    HIP_TRY(hipMalloc(&p, cap * sizeof(T)));
+    keep = b.p ? std::min(keep, b.n) : 0;  // nothing stored yet on the first growth
+    if (keep) HIP_TRY(hipMemcpyAsync(p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (b.p) (void)hipFree(b.p);
+    b.p = p;
+    b.n = cap;
+    return AID_OK;
+}
+
+extern "C" {
+
+int aid_dedup_reset(aid_engine *e) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->dd_n = 0;
+    e->dd_nw = 0;
+    return AID_OK;
+}
+
+int aid_dedup_count(aid_engine *e, int64_t *n_entries, int64_t *n_words) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    if (n_entries) *n_entries = e->dd_n;
+    if (n_words) *n_words = e->dd_nw;
+    return AID_OK;
+}
+
+static int check_offsets(const int64_t *off, int32_t n, const char *what) {
+    if (off[0] != 0) return fail(AID_ERR_INVALID, std::string(what) + ": offsets[0] must be 0");
+    for (int32_t i = 0; i < n; ++i)
+        if (off[i + 1] < off[i]) return fail(AID_ERR_INVALID, std::string(what) + ": offsets must be non-decreasing");
+    return AID_OK;
+}
+
+int aid_dedup_add(aid_engine *e, const uint32_t *words, const int64_t *offsets, const double *durations, int32_t n) {
+    if (!e || n < 0 || (n > 0 && (!offsets || !durations))) return fail(AID_ERR_INVALID, "aid_dedup_add: bad argument");
+    if (n == 0) return AID_OK;
+    if (int rc = check_offsets(offsets, n, "aid_dedup_add")) return rc;
+    const int64_t nw = offsets[n];
+    if (nw > 0 && !words) return fail(AID_ERR_INVALID, "aid_dedup_add: null words");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    if (int rc = grow_keep(e->dd_words, (size_t)e->dd_nw, (size_t)(e->dd_nw + nw + 1), s)) return rc;
+    if (int rc = grow_keep(e->dd_off, (size_t)e->dd_n + 1, (size_t)(e->dd_n + n + 1), s)) return rc;
+    if (int rc = grow_keep(e->dd_dur, (size_t)e->dd_n, (size_t)(e->dd_n + n), s)) return rc;
+    std::vector<int64_t> off(n + 1);
+    for (int32_t i = 0; i <= n; ++i) off[i] = e->dd_nw + offsets[i];
+    if (nw > 0) HIP_TRY(hipMemcpyAsync(e->dd_words.p + e->dd_nw, words, nw * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dd_off.p + e->dd_n, off.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dd_dur.p + e->dd_n, durations, n * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->dd_n += n;
+    e->dd_nw += nw;
+    return AID_OK;
+}
+
+int aid_dedup_scan(aid_engine *e, const uint32_t *words, const int64_t *offsets, const double *durations, int32_t nq,
+                   int64_t *best_idx, double *best_sim) {
+    if (!e || nq < 0 || (nq > 0 && (!offsets || !durations || !best_idx || !best_sim)))
+        return fail(AID_ERR_INVALID, "aid_dedup_scan: bad argument");
+    if (nq == 0) return AID_OK;
+    if (int rc = check_offsets(offsets, nq, "aid_dedup_scan")) return rc;
+    const int64_t nw = offsets[nq];
+    if (nw > 0 && !words) return fail(AID_ERR_INVALID, "aid_dedup_scan: null words");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    const int nc = std::max(1, dedup_chunks(e->dd_n));
+    std::vector<double> lo(nq), hi(nq);
+    for (int32_t q = 0; q < nq; ++q) {  // the reference's SQL bounds (dedup.py:193-194)
+        lo[q] = durations[q] * 0.9;
+        hi[q] = durations[q] * 1.1;
+    }
+    HIP_TRY(e->dq_words.reserve((size_t)nw + 1));
+    HIP_TRY(e->dq_off.reserve((size_t)nq + 1));
+    HIP_TRY(e->dq_lo.reserve((size_t)nq));
+    HIP_TRY(e->dq_hi.reserve((size_t)nq));
+    HIP_TRY(e->dq_sim.reserve((size_t)nq));
+    HIP_TRY(e->dq_idx.reserve((size_t)nq));
+    HIP_TRY(e->dq_psim.reserve((size_t)nq * nc));
+    HIP_TRY(e->dq_pidx.reserve((size_t)nq * nc));
+    if (nw > 0) HIP_TRY(hipMemcpyAsync(e->dq_words.p, words, nw * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dq_off.p, offsets, (nq + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dq_lo.p, lo.data(), nq * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dq_hi.p, hi.data(), nq * sizeof(double), hipMemcpyHostToDevice, s));
+    {
+        ProfScope ps(e, AID_K_DEDUP, s);
+        launch_dedup_scan(e->dd_words.p, e->dd_off.p, e->dd_dur.p, e->dd_n, e->dq_words.p, e->dq_off.p, e->dq_lo.p,
+                          e->dq_hi.p, nq, e->dq_psim.p, e->dq_pidx.p, e->dq_sim.p, e->dq_idx.p, s);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(best_idx, e->dq_idx.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(best_sim, e->dq_sim.p, nq * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return AID_OK;
+}
+
+int aid_dedup_pairs(aid_engine *e, const uint32_t *a, const int64_t *a_off, const uint32_t *b, const int64_t *b_off,
+                    int32_t n, double *sim) {
+    if (!e || n < 0 || (n > 0 && (!a_off || !b_off || !sim))) return fail(AID_ERR_INVALID, "aid_dedup_pairs: bad argument");
+    if (n == 0) return AID_OK;
+    if (int rc = check_offsets(a_off, n, "aid_dedup_pairs")) return rc;
+    if (int rc = check_offsets(b_off, n, "aid_dedup_pairs")) return rc;
+    const int64_t na = a_off[n], nb = b_off[n];
+    if ((na > 0 && !a) || (nb > 0 && !b)) return fail(AID_ERR_INVALID, "aid_dedup_pairs: null words");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    HIP_TRY(e->dq_words.reserve((size_t)na + 1));
+    HIP_TRY(e->dq_words2.reserve((size_t)nb + 1));
+    HIP_TRY(e->dq_off.reserve((size_t)n + 1));
+    HIP_TRY(e->dq_off2.reserve((size_t)n + 1));
+    HIP_TRY(e->dq_sim.reserve((size_t)n));
+    if (na > 0) HIP_TRY(hipMemcpyAsync(e->dq_words.p, a, na * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (nb > 0) HIP_TRY(hipMemcpyAsync(e->dq_words2.p, b, nb * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dq_off.p, a_off, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->dq_off2.p, b_off, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    launch_dedup_pairs(e->dq_words.p, e->dq_off.p, e->dq_words2.p, e->dq_off2.p, n, e->dq_sim.p, s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(sim, e->dq_sim.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return AID_OK;
 }
 
 int aid_profile_enable(aid_engine *e, int32_t on) {

@@ -25,6 +25,9 @@
 namespace aid {
 
 constexpr int kRowsPerStep = 4;
+#ifndef AID_K2_REVERSE
+#define AID_K2_REVERSE 1  // 1: last-written strips first (0.2975 -> 0.2930 ms, A/B on one box)
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
@@ -43,6 +46,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
         const int64_t nb = gridDim.x, b = blockIdx.x;
         const int64_t per = nb / 8, rem = nb % 8, x = b % 8, y = b / 8;
         strip = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
+#if AID_K2_REVERSE
+        strip = nb - 1 - strip;  // last-written power rows (still in the MALL after K1) first
+#endif
     }
     if (strip >= total_strips) return;
     int lo = 0, hi = n_clips - 1;

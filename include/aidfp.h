@@ -44,7 +44,8 @@ extern "C" {
 #define AID_K_SYNTH 4
 #define AID_K_MATCH 5
 #define AID_K_RESAMPLE 6
-#define AID_K_COUNT 7
+#define AID_K_DEDUP 7
+#define AID_K_COUNT 8
 
 typedef struct aid_engine aid_engine;
 
@@ -162,6 +163,23 @@ int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t
                        int32_t sr_out, int64_t m_first, int64_t count, float *dst, void *stream);
 /* (up, down, hl, J) of a rate pair (FPSPEC 8); returns 0 on bad rates */
 int aid_resample_plan(int32_t sr_in, int32_t sr_out, int32_t *up, int32_t *down, int32_t *hl, int32_t *J);
+
+/* ---- Chromaprint content dedup ----
+ * Replaces app/audio/dedup.py:127-222 (`_fingerprint_similarity`, `check_content_duplicate`):
+ * a device-resident catalog of raw Chromaprint fingerprints (u32 words) with durations; a scan
+ * scores every entry whose duration d satisfies lo <= d <= hi (lo = duration*0.9,
+ * hi = duration*1.1 in binary64, as the reference's SQL bounds) by
+ * (matching_bits / (min_len*32)) * (min_len / max_len) in binary64 and returns the best entry
+ * (earliest on ties, only scores > 0; -1 if none) and its score. Entry index = insertion order.
+ * All arrays are host arrays; offsets are int64[n+1] word offsets. */
+int aid_dedup_reset(aid_engine *e);
+int aid_dedup_add(aid_engine *e, const uint32_t *words, const int64_t *offsets, const double *durations, int32_t n);
+int aid_dedup_count(aid_engine *e, int64_t *n_entries, int64_t *n_words);
+int aid_dedup_scan(aid_engine *e, const uint32_t *words, const int64_t *offsets, const double *durations, int32_t nq,
+                   int64_t *best_idx, double *best_sim);
+/* score of n (a_i, b_i) pairs, same formula (the reference's `_fingerprint_similarity`) */
+int aid_dedup_pairs(aid_engine *e, const uint32_t *a, const int64_t *a_off, const uint32_t *b, const int64_t *b_off,
+                    int32_t n, double *sim);
 
 /* ---- native multi-GPU exchange (SURVEY.md 8b "aid_allgather_index", 8e) ----
  * One process per GPU. Rank 0 calls aid_comm_id, the host hands the 128 id bytes to every
