@@ -34,7 +34,7 @@ DEFAULT_THR = 4.0
 
 
 def build() -> Path:
-    srcs = [HERE / "fp_oracle.c", HERE / "fp_match.c", HERE / "fp_resample.c"]
+    srcs = [HERE / "fp_oracle.c", HERE / "fp_match.c", HERE / "fp_resample.c", HERE / "fp_dedup.c"]
     if not LIB_PATH.exists() or any(s.stat().st_mtime > LIB_PATH.stat().st_mtime for s in srcs):
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
@@ -91,6 +91,9 @@ def lib():
         L.fp_resample_len.argtypes = [i64, ctypes.c_int32, ctypes.c_int32]
         L.fp_resample.restype = i64
         L.fp_resample.argtypes = [P, i64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P]
+        L.fp_dedup_similarity.restype = ctypes.c_double
+        L.fp_dedup_similarity.argtypes = [P, i64, P, i64]
+        L.fp_dedup_scan.argtypes = [P, P, P, i64, P, P, P, i64, P, P]
         _lib = L
     return _lib
 
@@ -236,3 +239,25 @@ def resample(x: np.ndarray, sr_in: int, sr_out: int) -> np.ndarray:
     y = np.zeros(max(1, int(lib().fp_resample_len(n, sr_in, sr_out))), np.float32)
     m = lib().fp_resample(_ptr(x), n, ch, sr_in, sr_out, _ptr(y))
     return y[:m]
+
+
+# ---- Chromaprint dedup scan (dedup.py:127-222) ----
+def _pack_u32(arrs):
+    off = np.zeros(len(arrs) + 1, dtype=np.int64)
+    if arrs:
+        off[1:] = np.cumsum([len(a) for a in arrs])
+    w = np.concatenate(arrs).astype(np.uint32) if arrs and off[-1] else np.zeros(1, np.uint32)
+    return np.ascontiguousarray(w), off
+
+
+def dedup_scan(cat, cat_dur, queries, q_dur):
+    """cat/queries: lists of uint32 arrays. Returns (best_idx int64[nq] (-1 = none), best_sim f64[nq])."""
+    cw, co = _pack_u32(cat)
+    qw, qo = _pack_u32(queries)
+    cd = np.ascontiguousarray(cat_dur, dtype=np.float64)
+    qd = np.ascontiguousarray(q_dur, dtype=np.float64)
+    nq = len(queries)
+    bi = np.zeros(max(1, nq), np.int64)
+    bs = np.zeros(max(1, nq), np.float64)
+    lib().fp_dedup_scan(_ptr(cw), _ptr(co), _ptr(cd), len(cat), _ptr(qw), _ptr(qo), _ptr(qd), nq, _ptr(bi), _ptr(bs))
+    return bi[:nq], bs[:nq]

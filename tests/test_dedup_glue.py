@@ -31,3 +31,21 @@ def test_golden_file_shape():
     # the captured SQL bounds are the reference's duration*0.9 / duration*1.1
     for q in GOLD["queries"]:
         assert q["bounds"] == [q["duration"] * 0.9, q["duration"] * 1.1]
+
+
+def test_oracle_scan_reproduces_reference_decisions():
+    """oracle/fp_dedup.c (the CPU checker for big catalogs) against the reference's captured scans."""
+    import oracle as O
+
+    cat = [c for c in GOLD["catalog"] if c["fp"] is not None and c["duration"] is not None]
+    arrs = [dedup.parse_fingerprint(c["fp"]) for c in cat]
+    qs = [dedup.parse_fingerprint(q["fingerprint"]) for q in GOLD["queries"]]
+    bi, bs = O.dedup_scan(arrs, [c["duration"] for c in cat], qs, [q["duration"] for q in GOLD["queries"]])
+    for q, i, s in zip(GOLD["queries"], bi, bs):
+        got = cat[i]["id"] if i >= 0 and s >= q["threshold"] else None
+        assert got == q["result"]
+    for pair in GOLD["similarity"]:
+        a, b = dedup.parse_fingerprint(pair["fp1"]), dedup.parse_fingerprint(pair["fp2"])
+        if a is None or b is None:
+            continue
+        assert O.lib().fp_dedup_similarity(O._ptr(a), len(a), O._ptr(b), len(b)) == pair["sim"]
