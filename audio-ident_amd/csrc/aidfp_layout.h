@@ -13,9 +13,9 @@ constexpr int kZoneDF = 127;      // target zone, bins
 constexpr int kFan = 10;          // targets per anchor
 constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 
-// K1: 12 waves per workgroup, each wave slides over a strip of kStftStrip frames
+// K1: kStftWaves waves per workgroup (14: +2 % over 12 in same-box A/Bs), each wave slides over a strip of kStftStrip frames
 #ifndef AID_STFT_WAVES
-#define AID_STFT_WAVES 12
+#define AID_STFT_WAVES 14  // 14 x 8.5 KB exchange buffers + 32 KB tables fit the 160 KB LDS; VGPRs capped at 128
 #endif
 constexpr int kStftWaves = AID_STFT_WAVES;
 constexpr int kStftStrip = 16;

@@ -21,7 +21,7 @@
 //     (E3), then the real split reads each mirror pair (Z[k], Z[1024-k]) once
 //     (conflict-free) and produces both bins; stores are 64 consecutive bins per
 //     wave-instruction (the mirror bins in descending order, same 256-B segment).
-// A workgroup is 12 waves (3 per SIMD) sharing 32 KB of tables in LDS (float4 pairs,
+// A workgroup is kStftWaves = 14 waves (3-4 per SIMD, <= 128 VGPRs) sharing 32 KB of tables in LDS (float4 pairs,
 // read with ds_read_b128); the
 // exchanges are wave-private, so there is no workgroup barrier in the loop.
 #include "aidfp_device.h"
@@ -33,6 +33,11 @@
 //   9 = no stage A/B DFT16 arithmetic, 10 = one float stored per lane and frame (not 16 rows)
 #ifndef AID_K1_DIAG
 #define AID_K1_DIAG 0
+#endif
+// AID_K1_WINREG=1: the lane's 32 window values live in registers for the whole strip
+// (they do not change from frame to frame) instead of 8 ds_read_b128 per frame
+#ifndef AID_K1_WINREG
+#define AID_K1_WINREG 0
 #endif
 // AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
 // (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
@@ -108,6 +113,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     float2 ring[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) ring[r] = src[64 * r];
+#if AID_K1_WINREG
+    float4 wreg[8];
+#pragma unroll
+    for (int h = 0; h < 8; ++h) wreg[h] = s_win4[64 * h + lane];
+#endif
 
     for (int f0 = 0; f0 < nfr; f0 += PERIOD) {
 #pragma unroll
@@ -117,7 +127,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 float2 v[16];
 #pragma unroll
                 for (int h = 0; h < 8; ++h) {
+#if AID_K1_WINREG
+                    const float4 w = wreg[h];
+#else
                     const float4 w = s_win4[64 * h + lane];
+#endif
                     const float2 x0 = ring[(2 * h + ROWS * p) & 15], x1 = ring[(2 * h + 1 + ROWS * p) & 15];
                     v[2 * h] = make_float2(x0.x * w.x, x0.y * w.y);
                     v[2 * h + 1] = make_float2(x1.x * w.z, x1.y * w.w);
