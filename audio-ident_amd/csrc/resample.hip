@@ -6,7 +6,7 @@
 // store instruction writes 1 KB contiguous). It stages the input window those outputs touch
 // ONCE into LDS, downmixed to mono at staging time (float2 loads for stereo), zero outside the
 // clip; every output then runs its J-tap dot product from LDS with the phase row of the
-// [up][J] tap table (L1/L2-resident, a few KB to 54 KB). HBM traffic is the algorithmic
+// [up][J] tap table, itself staged in LDS when it fits 48 KB (else read from L1/L2). HBM traffic is the algorithmic
 // minimum: input once (+ the J-sample window overlap per block) and output once.
 #include "aidfp_device.h"
 
@@ -16,15 +16,25 @@ constexpr int kResThreads = 256;
 constexpr int kResPerThread = 4;
 constexpr int kResBlock = kResThreads * kResPerThread;
 
-template <bool STEREO>
+constexpr int kResMaxLdsTaps = 12288;  // floats (48 KB): larger tables are read from L1/L2
+
+// MODE 0: taps from L1/L2, 1: taps staged in LDS, 2: integer decimation (up == 1): one phase,
+// the taps are wave-uniform and read as scalar loads (no LDS traffic for them)
+template <bool STEREO, int MODE>
 __global__ __launch_bounds__(kResThreads) void k_resample(const float *__restrict__ src, int64_t in_base, int64_t n,
                                                          int up, int down, int hl, int J,
                                                          const float *__restrict__ taps, float *__restrict__ dst,
                                                          int64_t m_first, int64_t m_end) {
     // src[0] is stream sample in_base; samples outside [in_base, in_base + n) read as 0.
     // Outputs m_first .. m_end-1 (stream indices) go to dst[m - m_first].
-    extern __shared__ float sx[];
+    extern __shared__ float smem[];
     const int tid = threadIdx.x;
+    // [up][J] tap table first (when it fits), then the input window
+    constexpr bool LDS_TAPS = MODE == 1;
+    float *sx = LDS_TAPS ? smem + ((up * J + 3) & ~3) : smem;
+    if constexpr (LDS_TAPS) {
+        for (int i = tid; i < up * J; i += kResThreads) smem[i] = taps[i];
+    }
     const int64_t m0 = m_first + (int64_t)blockIdx.x * kResBlock;
     const int64_t mlast = min(m0 + kResBlock - 1, m_end - 1);
     const int64_t lo = (m0 * down + hl) / up - (J - 1);
@@ -49,17 +59,26 @@ __global__ __launch_bounds__(kResThreads) void k_resample(const float *__restric
         const int64_t m = m0 + tid + r * kResThreads;
         if (m >= m_end) break;
         const int64_t c = m * down + hl;
-        const int p = (int)(c % up);
-        const float *tp = taps + (int64_t)p * J;
-        const float *xp = sx + (c / up - lo);
         float acc = 0.0f;
-        for (int j = 0; j < J; ++j) acc = __builtin_fmaf(tp[j], xp[-j], acc);
+        if constexpr (MODE == 2) {
+            const float *xp = sx + (c - lo);
+            for (int j = 0; j < J; ++j) acc = __builtin_fmaf(taps[j], xp[-j], acc);  // taps[j]: uniform
+        } else {
+            const int p = (int)(c % up);
+            const float *tp = (LDS_TAPS ? smem : taps) + (int64_t)p * J;
+            const float *xp = sx + (c / up - lo);
+            for (int j = 0; j < J; ++j) acc = __builtin_fmaf(tp[j], xp[-j], acc);
+        }
         dst[m - m_first] = acc;
     }
 }
 
+static int64_t window_floats(int up, int down, int J) { return (int64_t)(kResBlock - 1) * down / up + J + 2; }
+
+static bool taps_in_lds(int up, int J) { return up > 1 && (int64_t)up * J <= kResMaxLdsTaps; }
+
 int64_t resample_lds_floats(int up, int down, int J) {
-    return (int64_t)(kResBlock - 1) * down / up + J + 2;
+    return window_floats(up, down, J) + (taps_in_lds(up, J) ? (((int64_t)up * J + 3) & ~3) : 0);
 }
 
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
@@ -68,11 +87,15 @@ void launch_resample(const float *src, int64_t in_base, int64_t n, int channels,
     const dim3 g((unsigned)((count + kResBlock - 1) / kResBlock)), b(kResThreads);
     const size_t lds = (size_t)resample_lds_floats(up, down, J) * sizeof(float);
     const int64_t m_end = m_first + count;
-    if (channels == 2)
-        hipLaunchKernelGGL(k_resample<true>, g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst, m_first, m_end);
-    else
-        hipLaunchKernelGGL(k_resample<false>, g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst, m_first,
-                           m_end);
+    const int mode = up == 1 ? 2 : taps_in_lds(up, J) ? 1 : 0;
+#define AID_RS_LAUNCH(ST, MD) \
+    hipLaunchKernelGGL((k_resample<ST, MD>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst, m_first, m_end)
+    if (channels == 2) {
+        if (mode == 2) AID_RS_LAUNCH(true, 2); else if (mode == 1) AID_RS_LAUNCH(true, 1); else AID_RS_LAUNCH(true, 0);
+    } else {
+        if (mode == 2) AID_RS_LAUNCH(false, 2); else if (mode == 1) AID_RS_LAUNCH(false, 1); else AID_RS_LAUNCH(false, 0);
+    }
+#undef AID_RS_LAUNCH
 }
 
 }  // namespace aid
