@@ -135,3 +135,22 @@ def test_back_to_back_calls_without_sync(gpu_engine):
     counts = gpu_engine.counts()
     assert counts.tolist() == [len(r) for r in ref_b]
     assert counts[1] == 0  # the 1000-sample clip has no frame
+
+
+@pytest.mark.parametrize("hop", [128, 256, 1024, 2048])
+def test_every_hop_bit_exact(hop):
+    """K1 is specialised per hop (hop/128 new PCM rows per frame): each specialisation is
+    bit-exact, power and hashes, including a long clip with several K3 chunks at hop 128."""
+    from aidfp.engine import Engine
+
+    with Engine(44100, hop=hop) as eng:
+        assert eng.hop == hop
+        lens = [2048, 2048 + hop * 37 + 5, 44100 * 3, 44100 * 7 + 1]
+        if hop == 128:
+            lens.append(2048 + 128 * 2500)  # 2501 frames: 3 K3 chunks
+        clips = [_clip(70 + i, n, start=101 * i, snr=25 if i % 2 else None) for i, n in enumerate(lens)]
+        got = eng.extract_host(clips)
+        for c, x in enumerate(clips):
+            P = eng.power(c, len(x))
+            assert np.array_equal(P.view(np.uint32), O.stft_power(x, hop).view(np.uint32)), (hop, c)
+            assert np.array_equal(got[c], O.fingerprint(x, hop)), (hop, c)
