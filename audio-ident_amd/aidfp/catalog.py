@@ -68,6 +68,7 @@ class IngestStats:
     t_build: float
     exchange: str = "none"
     t_comm_init: float = 0.0
+    t_synth: float = 0.0  # device time generating the synthetic PCM (inside t_extract's wall span)
 
 
 def native_comm(eng, group=None) -> int:
@@ -98,14 +99,21 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     t0 = time.perf_counter()
     pcm = torch.empty(max(1, min(batch, len(mine))) * n, dtype=torch.float32, device="cuda")
     base = eng.index_stats()["postings"]
+    s = torch.cuda.current_stream()
+    ev = []
     for b0 in range(0, len(mine), batch):
         tr = mine[b0 : b0 + batch]
-        eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
+        b.record(s)
+        ev.append((a, b))
         eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n)
         eng.index_add_extracted(tr)
     del pcm
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    t_synth = sum(a.elapsed_time(b) for a, b in ev) * 1e-3
     n_local = eng.index_stats()["postings"] - base
     total = n_local
     t_init = 0.0
@@ -141,4 +149,4 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     return IngestStats(len(mine), len(mine) * n / eng.sample_rate, n_local, total, t1 - t0 - t_init, t2 - t1,
-                       t3 - t2, exchange if world > 1 else "none", t_init)
+                       t3 - t2, exchange if world > 1 else "none", t_init, t_synth)

@@ -62,11 +62,13 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    phases = torch.tensor([wall, st.t_extract, st.t_exchange, st.t_build, st.t_comm_init], dtype=torch.float64,
-                          device="cuda")
+    # the synthetic tracks are generated on the device inside the extract span (SURVEY 8d config 3:
+    # "generated on device"); the ingest rate excludes that generation time, wall_s keeps it
+    phases = torch.tensor([wall - st.t_synth, st.t_extract - st.t_synth, st.t_exchange, st.t_build, st.t_comm_init,
+                           st.t_synth, wall], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(phases, op=dist.ReduceOp.MAX)
-    wall, te, tx, tb, ti = phases.tolist()
+    ingest, te, tx, tb, ti, tsyn, wall = phases.tolist()
 
     acc = None
     if rank == 0 and args.check:
@@ -82,8 +84,9 @@ def main() -> int:
         audio = args.tracks * args.seconds
         print(json.dumps({
             "metric": "catalog ingest audio-seconds/sec (extract + RCCL all-gather + index build), whole job",
-            "value": round(audio / wall, 1), "unit": "audio-s/s", "n_gpus": world, "tracks": args.tracks,
-            "track_seconds": args.seconds, "wall_s": round(wall, 3),
+            "value": round(audio / ingest, 1), "unit": "audio-s/s", "n_gpus": world, "tracks": args.tracks,
+            "track_seconds": args.seconds, "ingest_s": round(ingest, 3), "wall_s_with_generation": round(wall, 3),
+            "synth_generation_s": round(tsyn, 3),
             "phase_s_max_over_ranks": {"extract": round(te, 3), "allgather": round(tx, 3), "build": round(tb, 3),
                                        "comm_init": round(ti, 3)},
             "exchange": st.exchange,

@@ -29,8 +29,11 @@ def main() -> int:
     ap.add_argument("--tracks", type=int, default=1000)
     ap.add_argument("--minutes", type=float, default=10.0)
     ap.add_argument("--chunk-s", type=float, default=2.5)
+    ap.add_argument("--index-sr", type=int, default=48000,
+                    help="index rate; != 48000 resamples the stream on the GPU (16000 = the reference's Olaf rate)")
     args = ap.parse_args()
     SR = 48000
+    ISR = args.index_sr
     import torch
 
     from aidfp import synth
@@ -39,7 +42,7 @@ def main() -> int:
     from aidfp.stream import StreamIdentifier
 
     torch.cuda.set_device(0)
-    eng = Engine(SR, device=0)
+    eng = Engine(ISR, device=0)
     ingest_synthetic(eng, np.arange(args.tracks, dtype=np.uint32), 30.0)
     rng = np.random.default_rng(42)
     seg = 30 * SR
@@ -49,12 +52,12 @@ def main() -> int:
     right = np.concatenate([synth.synth(int(t), 0, seg, SR, snr_db=30.0, salt=12) for t in seg_tracks])
     stereo = np.stack([left, right], axis=1)
 
-    sid = StreamIdentifier(eng)
+    sid = StreamIdentifier(eng, stream_sr=SR)
     chunk = int(args.chunk_s * SR)
     lat = []
     results = []
     sid.push(stereo[:chunk])  # warm-up (first allocations)
-    sid = StreamIdentifier(eng)
+    sid = StreamIdentifier(eng, stream_sr=SR)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for a in range(0, len(stereo), chunk):
@@ -66,7 +69,7 @@ def main() -> int:
     ok = n = 0
     for r in results:
         s0 = int(round(r.start_s * SR))
-        si, sj = s0 // seg, (s0 + sid.win - 1) // seg
+        si, sj = s0 // seg, (s0 + int(round(sid.win * SR / ISR)) - 1) // seg
         if si != sj:
             continue
         n += 1
@@ -74,6 +77,7 @@ def main() -> int:
     stream_s = len(stereo) / SR
     print(json.dumps({
         "metric": "48 kHz stereo stream, 5 s / 2.5 s windows: sustained audio-s/s, 1 GPU",
+        "index_sr": ISR, "front_end": "downmix" if ISR == SR else f"downmix + resample 48000 -> {ISR} (K6)",
         "value": round(stream_s / total, 1), "unit": "audio-s/s", "n_gpus": 1,
         "stream_s": stream_s, "windows": len(results), "chunk_s": args.chunk_s,
         "push_latency_ms": {p: round(1e3 * float(np.percentile(lat, q)), 3) for p, q in (("p50", 50), ("p95", 95), ("p99", 99))},
