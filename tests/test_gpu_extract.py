@@ -154,3 +154,16 @@ def test_every_hop_bit_exact(hop):
             P = eng.power(c, len(x))
             assert np.array_equal(P.view(np.uint32), O.stft_power(x, hop).view(np.uint32)), (hop, c)
             assert np.array_equal(got[c], O.fingerprint(x, hop)), (hop, c)
+
+
+def test_max_duration_clip(gpu_engine):
+    """The reference accepts uploads up to 1800 s (decode.py `decode_and_validate`
+    max_duration): one 30-minute clip (155k frames, 152 K3 chunks) next to short ones."""
+    long = _clip(123, SR * 1800, start=0, snr=30)
+    clips = [_clip(1, 5000), long, _clip(2, SR * 5)]
+    got = gpu_engine.extract_host(clips)
+    for c, x in enumerate(clips):
+        r = O.fingerprint(x, HOP)
+        assert len(got[c]) == len(r), c
+        assert np.array_equal(got[c], r), c
+    assert len(got[1]) > 100000
