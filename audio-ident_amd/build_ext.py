@@ -32,10 +32,15 @@ FLAGS = [
     "-Wall",
     "-Wno-unused-result",
 ]
+# Per-file flags. K1 is complex arithmetic whose DFT4 mixes re/im across lanes of a float2: hipcc's
+# SLP vectorizer packs it into v_pk_*_f32 (4 cycles each on gfx950, the rate of two scalar ops) plus
+# ~134 v_mov per frame to shuffle pairs; scalar code is 20 % fewer VALU cycles (K1 0.464 -> 0.419 ms,
+# same-box A/B). K2 is the opposite (0.290 -> 0.329 without SLP), so this stays per file.
+FILE_FLAGS = {"stft.hip": ["-fno-slp-vectorize"]}
 
 
 def _deps(src: Path) -> list[Path]:
-    return [src] + sorted(CSRC.glob("*.h")) + [PKG.parent / "include" / "aidfp.h"]
+    return [src, Path(__file__)] + sorted(CSRC.glob("*.h")) + [PKG.parent / "include" / "aidfp.h"]
 
 
 def _compile(name: str, verbose: bool, objdir: Path = OBJ, extra: tuple = ()) -> Path:
@@ -43,22 +48,23 @@ def _compile(name: str, verbose: bool, objdir: Path = OBJ, extra: tuple = ()) ->
     obj = objdir / (name + ".o")
     if obj.exists() and all(d.stat().st_mtime <= obj.stat().st_mtime for d in _deps(src)):
         return obj
-    cmd = [HIPCC, *FLAGS, *extra, "-c", str(src), "-o", str(obj)]
+    flags = [*FLAGS, *FILE_FLAGS.get(name, []), *extra]
+    cmd = [HIPCC, *flags, "-c", str(src), "-o", str(obj)]
     if name.endswith(".cpp"):
-        cmd = [HIPCC, *FLAGS, *extra, "-x", "hip", "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *flags, "-x", "hip", "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     return obj
 
 
-def build(verbose: bool = False, variant: str | None = None, defines: tuple = ()) -> Path:
+def build(verbose: bool = False, variant: str | None = None, defines: tuple = (), flags: tuple = ()) -> Path:
     """Build the product library; `variant` builds a diagnostic copy (build/<variant>/libaidfp.so)
     with extra -D defines, used only for profiling experiments (never loaded by default)."""
     objdir = OBJ if variant is None else OBJ / variant
     lib = LIB if variant is None else objdir / "libaidfp.so"
     objdir.mkdir(parents=True, exist_ok=True)
-    extra = tuple(f"-D{d}" for d in defines)
+    extra = tuple(f"-D{d}" for d in defines) + tuple(flags)
     srcs = [s for s in SOURCES if (CSRC / s).exists()]
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, verbose, objdir, extra), srcs))

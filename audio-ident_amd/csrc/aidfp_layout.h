@@ -25,7 +25,10 @@ constexpr int kStftStrip = 16;
 constexpr int kStftLdsPerWave = AID_K1_COMPACT ? 1024 : 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024)
 
 // K2: output frames per workgroup strip
-constexpr int kPeakStrip = 128;
+#ifndef AID_PEAK_STRIP
+#define AID_PEAK_STRIP 128
+#endif
+constexpr int kPeakStrip = AID_PEAK_STRIP;
 
 // K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
 constexpr int kHashChunk = 1024;

@@ -28,6 +28,9 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_REVERSE
 #define AID_K2_REVERSE 1  // 1: last-written strips first (0.2975 -> 0.2930 ms, A/B on one box)
 #endif
+#ifndef AID_K2_PF
+#define AID_K2_PF 4  // prefetch distance in rows (4 or 8): rows it+PF .. are in flight in registers
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
@@ -91,9 +94,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
     const int64_t rbeg = t0 - kPeakDT;
     const int iters = (int)(t1 - t0) + 2 * kPeakDT;
-    float4 pf[kRowsPerStep];  // rows of the next batch, in flight
+    float4 pf[AID_K2_PF];  // rows of the next batch(es), in flight
 #pragma unroll
-    for (int j = 0; j < kRowsPerStep; ++j) {
+    for (int j = 0; j < AID_K2_PF; ++j) {
         const int64_t r = rbeg + j;
         pf[j] = (j < iters && r >= 0 && r < F) ? reinterpret_cast<const float4 *>(P + r * kBins)[tid]
                                                : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -110,11 +113,12 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll
                 for (int j = 0; j < kRowsPerStep; ++j) {
-                    reinterpret_cast<float4 *>(&rows[buf][j][16])[tid] = pf[j];
-                    const int64_t rn = rbeg + it + j + kRowsPerStep;
-                    pf[j] = (it + j + kRowsPerStep < iters && rn >= 0 && rn < F)
-                                ? reinterpret_cast<const float4 *>(P + rn * kBins)[tid]
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                    const int slot = (s + j) % AID_K2_PF;  // compile-time: the loop is unrolled by 8
+                    reinterpret_cast<float4 *>(&rows[buf][j][16])[tid] = pf[slot];
+                    const int64_t rn = rbeg + it + j + AID_K2_PF;
+                    pf[slot] = (it + j + AID_K2_PF < iters && rn >= 0 && rn < F)
+                                   ? reinterpret_cast<const float4 *>(P + rn * kBins)[tid]
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
                 __syncthreads();
             }
