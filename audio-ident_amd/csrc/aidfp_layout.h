@@ -24,11 +24,31 @@ constexpr int kStftStrip = 16;
 #endif
 constexpr int kStftLdsPerWave = AID_K1_COMPACT ? 1024 : 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024)
 
-// K2: output frames per workgroup strip
-#ifndef AID_PEAK_STRIP
-#define AID_PEAK_STRIP 128
+// K2: output frames per workgroup strip, sized per call (peak_strip_len) between these bounds
+#ifndef AID_PEAK_STRIP_MIN
+#define AID_PEAK_STRIP_MIN 64  // shorter strips re-read too much halo (14 rows per strip)
 #endif
-constexpr int kPeakStrip = AID_PEAK_STRIP;
+constexpr int kPeakStripMin = AID_PEAK_STRIP_MIN;
+
+// Smallest strip length L >= kPeakStripMin with sum_c ceil(F_c / L) <= slots (the resident K2
+// workgroups of the device): every strip then runs in the first (only) round. When the clips
+// alone outnumber the slots, L = max F (one strip per clip).
+inline int peak_strip_len(const int64_t *frames, int n, int64_t slots) {
+    int64_t fmax = 0;
+    for (int c = 0; c < n; ++c) fmax = frames[c] > fmax ? frames[c] : fmax;
+    auto count = [&](int64_t L) {
+        int64_t k = 0;
+        for (int c = 0; c < n; ++c) k += (frames[c] + L - 1) / L;
+        return k;
+    };
+    int64_t lo = kPeakStripMin, hi = fmax > lo ? fmax : lo;
+    if (count(lo) <= slots) return (int)lo;
+    while (lo < hi) {  // count(L) is non-increasing in L
+        const int64_t mid = (lo + hi) / 2;
+        if (count(mid) <= slots) hi = mid; else lo = mid + 1;
+    }
+    return (int)lo;
+}
 
 // K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
 constexpr int kHashChunk = 1024;

@@ -24,7 +24,8 @@
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_strips, int hop,
                        const Tables *tab, float *out, bool logmag, hipStream_t s);
-void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, float thr,
+int peak_pick_blocks_per_cu();
+void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
                       uint64_t *mask, hipStream_t s);
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s);
@@ -170,6 +171,7 @@ struct aid_engine {
     std::vector<int64_t> clip_frames;
     int n_clips = 0;
     int64_t total_frames = 0, total_strips = 0, total_chunks = 0, total_records = 0;
+    int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
     hipStream_t last_stream = nullptr;
     bool have_result = false;
 
@@ -273,6 +275,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     aid_engine *e = new aid_engine();
     e->cfg = c;
     e->device = dev;
+    e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
     if (he != hipSuccess) {
         delete e;
@@ -403,6 +406,8 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
     e->clip_frames.assign(n_clips, 0);
     int64_t frames = 0, strips = 0, chunks = 0, recs = 0, staged = 0, kstrips = 0;
     bool empty_clip = false;  // a clip without frames gets no count from K3: zero the counts first
+    for (int c = 0; c < n_clips; ++c) e->clip_frames[c] = num_frames(offsets[c + 1] - offsets[c], hop);
+    const int strip_len = peak_strip_len(e->clip_frames.data(), n_clips, e->k2_slots);
     for (int c = 0; c < n_clips; ++c) {
         const int64_t n = offsets[c + 1] - offsets[c];
         const int64_t F = num_frames(n, hop);
@@ -425,7 +430,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         e->clip_frames[c] = F;
         empty_clip |= F == 0;
         frames += F;
-        strips += (F + kPeakStrip - 1) / kPeakStrip;
+        strips += (F + strip_len - 1) / strip_len;
         chunks += (F + kHashChunk - 1) / kHashChunk;
         recs += d.hash_cap;
         kstrips += (F + kStftStrip - 1) / kStftStrip;
@@ -478,7 +483,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         }
         {
             ProfScope ps(e, AID_K_PEAKS, s);
-            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, e->cfg.peak_threshold, e->mask.p, s);
+            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->mask.p, s);
         }
         if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s);

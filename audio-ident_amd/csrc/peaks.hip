@@ -4,8 +4,11 @@
 // Replaces the spectral-peak stage inside the external `olaf_c` binary
 // (reference call sites fingerprint.py:117-125, 185-193).
 //
-// One workgroup streams one strip of kPeakStrip output frames of one clip and
-// reads every power row of the strip (+7 halo rows each side) once:
+// One workgroup streams one strip of `strip_len` output frames of one clip and
+// reads every power row of the strip (+7 halo rows each side) once. The host sizes
+// strip_len per call so the strips fill the resident workgroup slots in one round
+// (peak_strip_len); a fixed 128-frame strip left a third round 1/3 full at 256 x 10 s:
+//
 //   * thread j owns bins 4j..4j+3 (one float4 load per row); the next batch of 4
 //     rows is in flight in registers while the current one is processed;
 //   * rows are staged in LDS 4 at a time (double-buffered, one barrier per 4
@@ -36,7 +39,7 @@ constexpr int kRowsPerStep = 4;
 #endif
 
 __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
-                                                  int n_clips, int64_t total_strips, float thr,
+                                                  int n_clips, int64_t total_strips, int strip_len, float thr,
                                                   uint64_t *__restrict__ mask) {
     __shared__ __attribute__((aligned(16))) float rows[2][kRowsPerStep][kBins + 32];
     const int tid = threadIdx.x;
@@ -61,8 +64,8 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     }
     const int64_t F = clips[lo].frames;
     const int64_t fb = clips[lo].frame_base;
-    const int64_t t0 = (strip - clips[lo].strip_base) * kPeakStrip;
-    const int64_t t1 = min(t0 + (int64_t)kPeakStrip, F);
+    const int64_t t0 = (strip - clips[lo].strip_base) * strip_len;
+    const int64_t t1 = min(t0 + (int64_t)strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
 
@@ -179,11 +182,18 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     }
 }
 
-void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, float thr,
-                      uint64_t *mask, hipStream_t s) {
+void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
+                      float thr, uint64_t *mask, hipStream_t s) {
     if (total_strips <= 0) return;
     hipLaunchKernelGGL(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
-                       thr, mask);
+                       strip_len, thr, mask);
+}
+
+// resident K2 workgroups per CU (registers / LDS), for sizing strips to one round
+int peak_pick_blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_peak_pick, 256, 0) != hipSuccess || n <= 0) n = 1;
+    return n;
 }
 
 }  // namespace aid
