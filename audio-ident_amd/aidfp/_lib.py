@@ -61,6 +61,15 @@ class AidMatchRow(ctypes.Structure):
     ]
 
 
+class AidExactRow(ctypes.Structure):
+    _fields_ = [
+        ("track", ctypes.c_uint32),
+        ("aligned_hashes", ctypes.c_int32),
+        ("offset_seconds", ctypes.c_double),
+        ("confidence", ctypes.c_double),
+    ]
+
+
 # (name, restype, argtypes) for every symbol include/aidfp.h declares
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
@@ -98,6 +107,8 @@ SIGNATURES = [
     ("aid_index_load", ctypes.c_int, [P, ctypes.c_char_p]),
     ("aid_query", ctypes.c_int, [P, P, P, I32, P, P]),
     ("aid_query_extracted", ctypes.c_int, [P, P, P]),
+    ("aid_exact_lane", ctypes.c_int, [P, P, P, I32, I32, I32, P, P, P]),
+    ("aid_exact_windows", ctypes.c_int, [I64, I32, P, P, P]),
     ("aid_downmix", ctypes.c_int, [P, P, I64, P, P]),
     ("aid_resample_len", I64, [I64, I32, I32]),
     ("aid_resample", ctypes.c_int, [P, P, I64, I32, I32, I32, P, I64, P, P]),

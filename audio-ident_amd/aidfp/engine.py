@@ -291,6 +291,36 @@ class Engine:
         check(self._lib.aid_query_extracted(self._h, ctypes.addressof(rows), _p(nrows)))
         return self._rows(rows, nrows, nq)
 
+    # -- batched exact lane --
+    EXACT_DTYPE = np.dtype([("track", "<u4"), ("aligned_hashes", "<i4"), ("offset_seconds", "<f8"),
+                            ("confidence", "<f8")])
+
+    def exact_lane(self, clips: Sequence[np.ndarray] | None = None, max_out: int = 0, *, pcm_ptr: int = 0,
+                   offsets: np.ndarray | None = None) -> list[np.ndarray]:
+        """Sub-window fan-out + match + consensus + ranking for a batch of clips (aid_exact_lane).
+
+        Host clips, or device PCM (pcm_ptr) with host offsets. Returns per clip a structured array
+        (track, aligned_hashes, offset_seconds, confidence) in rank order, at most max_out rows
+        (default 3 x max_results: every candidate the consensus can keep)."""
+        max_out = int(max_out) or 3 * self.max_results
+        if clips is not None:
+            arrs = [np.ascontiguousarray(c, dtype=np.float32).ravel() for c in clips]
+            offsets = np.zeros(len(arrs) + 1, dtype=np.int64)
+            if arrs:
+                offsets[1:] = np.cumsum([len(a) for a in arrs])
+            pcm = np.concatenate(arrs) if arrs and offsets[-1] else np.zeros(1, dtype=np.float32)
+            src, loc = _p(pcm), AID_PCM_HOST
+        else:
+            offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+            src, loc = ctypes.c_void_p(pcm_ptr), AID_PCM_DEVICE
+        n = len(offsets) - 1
+        if n <= 0:
+            return []
+        out = np.zeros(n * max_out, dtype=self.EXACT_DTYPE)
+        nout = np.zeros(n, dtype=np.int32)
+        check(self._lib.aid_exact_lane(self._h, src, _p(offsets), n, loc, max_out, _p(out), _p(nout), None))
+        return [out[c * max_out: c * max_out + nout[c]].copy() for c in range(n)]
+
     def downmix(self, stereo_ptr: int, n_frames: int, mono_ptr: int, stream: int | None = None) -> None:
         check(self._lib.aid_downmix(self._h, ctypes.c_void_p(stereo_ptr), int(n_frames), ctypes.c_void_p(mono_ptr),
                                     ctypes.c_void_p(stream) if stream else None))
@@ -304,6 +334,17 @@ class Engine:
         n = np.zeros(L.AID_K_COUNT, dtype=np.int64)
         check(self._lib.aid_profile_read(self._h, _p(ms), _p(n), 1 if reset else 0))
         return {name: (float(ms[i]), int(n[i])) for i, name in enumerate(L.KERNEL_NAMES)}
+
+
+def exact_windows(n: int, sample_rate: int) -> tuple[int, list[tuple[int, int]]]:
+    """The exact lane's window plan for a clip of n samples (host only): (mode, [(lo, len)])."""
+    lo = np.zeros(3, dtype=np.int64)
+    ln = np.zeros(3, dtype=np.int64)
+    mode = np.zeros(1, dtype=np.int32)
+    k = L.load().aid_exact_windows(int(n), int(sample_rate), _p(lo), _p(ln), _p(mode))
+    if k < 0:
+        raise EngineError(k, L.last_error())
+    return int(mode[0]), [(int(lo[w]), int(ln[w])) for w in range(k)]
 
 
 def peaks_from_mask(mask: np.ndarray) -> np.ndarray:

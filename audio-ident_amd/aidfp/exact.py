@@ -56,14 +56,14 @@ class ExactMatch:
     aligned_hashes: int
 
 
-def pcm_duration_sec(pcm: bytes) -> float:
-    return (len(pcm) // BYTES_PER_SAMPLE) / SAMPLE_RATE
+def pcm_duration_sec(pcm: bytes, sample_rate: int = SAMPLE_RATE) -> float:
+    return (len(pcm) // BYTES_PER_SAMPLE) / sample_rate
 
 
-def extract_pcm_window(pcm: bytes, start_sec: float, stop_sec: float) -> bytes:
+def extract_pcm_window(pcm: bytes, start_sec: float, stop_sec: float, sample_rate: int = SAMPLE_RATE) -> bytes:
     """Byte slice [start, stop) at 16 kHz f32le, clamped to the data (reference :374-399)."""
-    lo = int(start_sec * SAMPLE_RATE) * BYTES_PER_SAMPLE
-    hi = int(stop_sec * SAMPLE_RATE) * BYTES_PER_SAMPLE
+    lo = int(start_sec * sample_rate) * BYTES_PER_SAMPLE
+    hi = int(stop_sec * sample_rate) * BYTES_PER_SAMPLE
     lo = min(max(lo, 0), len(pcm))
     hi = max(lo, min(hi, len(pcm)))
     return pcm[lo:hi]
@@ -174,13 +174,56 @@ async def enrich(top: list[ScoredCandidate], lookup: LookupFn) -> list[ExactMatc
 
 async def run_exact_lane(pcm_16k: bytes, max_results: int = 10, *, query: QueryFn | None = None,
                          lookup: LookupFn | None = None) -> list[ExactMatch]:
-    """Reference semantics of run_exact_lane (exact.py:70-124) over the GPU engine."""
+    """Reference semantics of run_exact_lane (exact.py:70-124) over the GPU engine.
+
+    With the default query function the whole lane (fan-out, match, consensus, ranking) is one
+    batched engine call (run_exact_lane_batch); an injected `query` runs the per-window path."""
     if not pcm_16k:
         return []
-    q = query or _default_query
+    if query is None:
+        return (await run_exact_lane_batch([pcm_16k], max_results, lookup=lookup))[0]
     duration = pcm_duration_sec(pcm_16k)
     if duration <= SHORT_CLIP_THRESHOLD_SEC:
-        scored = await _query_subwindows(pcm_16k, duration, q)
+        scored = await _query_subwindows(pcm_16k, duration, query)
     else:
-        scored = await _query_full(pcm_16k, q)
+        scored = await _query_full(pcm_16k, query)
     return await enrich(rank(scored, max_results), lookup or _default_lookup)
+
+
+def candidates_from_rows(rows, names: dict[int, str], max_results: int) -> list[ScoredCandidate]:
+    """Engine exact-lane rows (rank order) -> ScoredCandidate list: rows of tracks without a name
+    (not in the service's map) are dropped before the top-N cut, as the per-window path drops
+    them before the consensus (a track is its own group, so the survivors' order is the same)."""
+    out = []
+    for r in rows:
+        name = names.get(int(r["track"]))
+        tid = _as_uuid(name) if name is not None else None
+        if tid is None:
+            continue
+        out.append(ScoredCandidate(tid, int(r["aligned_hashes"]), float(r["offset_seconds"]), float(r["confidence"])))
+        if len(out) == max_results:
+            break
+    return out
+
+
+async def run_exact_lane_batch(clips: Sequence[bytes], max_results: int = 10, *, service=None,
+                               lookup: LookupFn | None = None) -> list[list[ExactMatch]]:
+    """run_exact_lane for a batch of 16 kHz f32le clips in one engine call (aid_exact_lane):
+    sub-window fan-out, K1-K5 and the consensus/threshold/ranking kernel on the GPU; only the
+    metadata lookup runs here. An engine failure gives [] for every clip (the reference logs a
+    failed olaf query and carries on, exact.py:163-171)."""
+    import asyncio
+
+    from .fingerprint import get_service
+
+    svc = service or get_service()
+    if not clips:
+        return []
+    try:
+        ranked = await asyncio.get_running_loop().run_in_executor(None, svc.exact_batch, list(clips), max_results)
+    except OlafError:
+        raise
+    except Exception:
+        logger.exception("batched exact lane failed")
+        ranked = [[] for _ in clips]
+    return [await enrich(r, lookup or _default_lookup) for r in ranked]

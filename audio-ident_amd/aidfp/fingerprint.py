@@ -190,6 +190,22 @@ class FingerprintService:
             out.sort(key=lambda m: m.match_count, reverse=True)
             return out
 
+    def exact_batch(self, clips: list[bytes], max_results: int) -> list[list]:
+        """Batched exact lane over the engine (aid_exact_lane); ranked ScoredCandidate lists."""
+        from ._lib import EngineError
+        from .exact import candidates_from_rows
+
+        with self._lock:
+            eng = self._eng()
+            pcms = [self._pcm(c) for c in clips]
+            try:
+                rows = eng.exact_lane(pcms)
+            except EngineError as exc:
+                logger.error("aidfp exact lane failed: %s", exc)
+                return [[] for _ in clips]
+            return [candidates_from_rows(r, self._names, max_results) if len(p) else []
+                    for r, p in zip(rows, pcms)]
+
     def delete_track(self, name: str) -> bool:
         from ._lib import EngineError
 

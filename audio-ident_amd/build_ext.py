@@ -21,7 +21,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "stream.hip", "resample.hip",
-           "dedup.hip", "engine.cpp"]
+           "dedup.hip", "exact.hip", "engine.cpp"]
 FLAGS = [
     f"--offload-arch={ARCH}",
     "-O3",

@@ -57,6 +57,10 @@ void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t
                       int min_match, int max_rows, int32_t *rows, int32_t *nrows, hipStream_t s);
 uint32_t index_keys();
 void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
+void launch_window_gather(const float *src, const int64_t *win, int n_win, int64_t max_len, float *dst, hipStream_t s);
+void launch_exact_consensus(const int32_t *rows, const int32_t *nrows, int mr, const int32_t *clip_win, int n_clips,
+                            double sec, int max_out, void *out, int32_t *n_out, hipStream_t s);
+void launch_rows_scatter(const int32_t *src, const int32_t *order, int n, int mr, int32_t *dst, hipStream_t s);
 }  // namespace aid
 
 using namespace aid;
@@ -145,6 +149,11 @@ struct aid_engine {
     DevBuf<uint32_t> q_hist;
     DevBuf<int32_t> q_rows, q_nrows;
     DevBuf<int64_t> x_src, x_dst;
+    // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
+    DevBuf<float> x_in, x_win;
+    DevBuf<int64_t> x_wdesc;
+    DevBuf<int32_t> x_order, x_clipwin, x_nout;
+    DevBuf<double> x_out;  // aid_exact_row, 3 x 8 bytes each
     DevBuf<int64_t> g_meta;            // all-gather: (count, n_tracks) per rank
     std::map<std::pair<int32_t, int32_t>, float *> rs_taps;  // (up, down) -> device [up][J] taps
     // Chromaprint dedup catalog (insertion order) + scan scratch
@@ -334,6 +343,13 @@ void aid_engine_destroy(aid_engine *e) {
     e->q_nrows.release();
     e->x_src.release();
     e->x_dst.release();
+    e->x_in.release();
+    e->x_win.release();
+    e->x_wdesc.release();
+    e->x_order.release();
+    e->x_clipwin.release();
+    e->x_nout.release();
+    e->x_out.release();
     e->g_meta.release();
     for (auto &kv : e->rs_taps) (void)hipFree(kv.second);
     e->dd_words.release();
@@ -371,6 +387,9 @@ int64_t aid_num_frames(const aid_engine *e, int64_t n) { return e ? num_frames(n
 
 int64_t aid_hash_capacity(const aid_engine *e, int64_t n) { return e ? hash_capacity(num_frames(n, e->cfg.hop)) : 0; }
 
+static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
+                          void *stream);
+
 int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc, void *stream) {
     if (!e || !offsets || n_clips < 0) return fail(AID_ERR_INVALID, "aid_extract: bad argument");
     if (loc != AID_PCM_HOST && loc != AID_PCM_DEVICE) return fail(AID_ERR_INVALID, "aid_extract: bad pcm_location");
@@ -379,6 +398,11 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         if (offsets[c + 1] < offsets[c] || offsets[c] < 0)
             return fail(AID_ERR_INVALID, "aid_extract: offsets must be non-decreasing and >= 0");
     std::lock_guard<std::mutex> lk(e->mu);
+    return extract_locked(e, pcm, offsets, n_clips, loc, stream);
+}
+
+static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
+                          void *stream) {
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = pick_stream(e, stream);
     const int hop = e->cfg.hop;
@@ -1231,6 +1255,8 @@ int aid_index_load(aid_engine *e, const char *path) {
 // run K5 over nq queries whose records are at device ranges (q_start/q_count device arrays).
 // max_recs = the largest query (host-known); the vote histogram gets ~8 buckets per
 // expected vote; queries whose exact LDS table overflowed are re-run with 4x the buckets.
+// rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
+// nrows (host) is always filled
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
                        int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
     const int mr = e->cfg.max_results;
@@ -1261,7 +1287,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         }
         HIP_TRY(hipGetLastError());
         std::vector<int32_t> got_n(nq);
-        HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        if (rows)
+            HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(got_n.data(), e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         std::vector<int> again;
@@ -1308,8 +1335,16 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             HIP_TRY(hipGetLastError());
         }
         std::vector<int32_t> got_n(n);
-        std::vector<aid_match_row> got((size_t)n * mr);
-        HIP_TRY(hipMemcpyAsync(got.data(), out_rows, (size_t)n * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        std::vector<aid_match_row> got;
+        if (rows) {
+            got.resize((size_t)n * mr);
+            HIP_TRY(hipMemcpyAsync(got.data(), out_rows, (size_t)n * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        } else {  // device mode: the batch's rows go to their queries' slots of q_rows
+            HIP_TRY(e->x_order.reserve(order.size()));
+            HIP_TRY(hipMemcpyAsync(e->x_order.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+            launch_rows_scatter(out_rows, e->x_order.p, n, mr, e->q_rows.p, s);
+            HIP_TRY(hipGetLastError());
+        }
         HIP_TRY(hipMemcpyAsync(got_n.data(), out_n, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         std::vector<int> again;
@@ -1320,7 +1355,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
                 continue;
             }
             nrows[q] = got_n[i];
-            std::memcpy(rows + (size_t)q * mr, got.data() + (size_t)i * mr, (size_t)mr * sizeof(aid_match_row));
+            if (rows) std::memcpy(rows + (size_t)q * mr, got.data() + (size_t)i * mr, (size_t)mr * sizeof(aid_match_row));
         }
         todo.swap(again);
     }
@@ -1383,3 +1418,118 @@ extern "C" int aid_downmix(aid_engine *e, const float *stereo, int64_t n_frames,
     HIP_TRY(hipGetLastError());
     return AID_OK;
 }
+
+// ---------------------------------------------------------------- batched exact lane
+
+extern "C" int aid_exact_windows(int64_t n, int32_t sample_rate, int64_t *lo, int64_t *len, int32_t *mode) {
+    if (n < 0 || sample_rate <= 0 || !lo || !len || !mode) return fail(AID_ERR_INVALID, "aid_exact_windows: bad argument");
+    // app/search/exact.py: duration = samples / SAMPLE_RATE (:389-390); <= 5.0 s -> SUB_WINDOWS
+    // (:48-52, :103), stop = min(b, duration), piece = _extract_pcm_window(a, stop) if a < stop
+    // (:150-160), whose byte bounds are int(t * SAMPLE_RATE) * 4 clamped to the data (:374-399)
+    static const double kSub[3][2] = {{0.0, 3.5}, {0.75, 4.25}, {1.5, 5.0}};
+    const double sr = (double)sample_rate, dur = (double)n / sr;
+    if (!(dur <= 5.0)) {
+        *mode = 0;
+        lo[0] = 0;
+        len[0] = n;
+        return 1;
+    }
+    *mode = 1;
+    for (int w = 0; w < 3; ++w) {
+        const double a = kSub[w][0], stop = std::min(kSub[w][1], dur);
+        int64_t l = 0, h = 0;
+        if (a < stop) {
+            l = std::min(std::max<int64_t>((int64_t)(a * sr), 0), n);
+            h = std::max(l, std::min<int64_t>((int64_t)(stop * sr), n));
+        }
+        lo[w] = l;
+        len[w] = h - l;  // 0: the reference sends no query for this window
+    }
+    return 3;
+}
+
+extern "C" int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
+                              int32_t max_out, aid_exact_row *out, int32_t *n_out, void *stream) {
+    if (!e || !offsets || n_clips < 0 || max_out <= 0 || (n_clips > 0 && (!out || !n_out)))
+        return fail(AID_ERR_INVALID, "aid_exact_lane: bad argument");
+    if (loc != AID_PCM_HOST && loc != AID_PCM_DEVICE) return fail(AID_ERR_INVALID, "aid_exact_lane: bad pcm_location");
+    for (int c = 0; c < n_clips; ++c)
+        if (offsets[c + 1] < offsets[c] || offsets[c] < 0)
+            return fail(AID_ERR_INVALID, "aid_exact_lane: offsets must be non-decreasing and >= 0");
+    if (n_clips > 0 && !pcm && offsets[n_clips] > offsets[0]) return fail(AID_ERR_INVALID, "aid_exact_lane: null pcm");
+    if (e->cfg.max_results > 256) return fail(AID_ERR_INVALID, "aid_exact_lane: engine max_results must be <= 256");
+    if (n_clips == 0) return AID_OK;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    if (int rc = ensure_index(e)) return rc;
+    hipStream_t s = pick_stream(e, stream);
+    if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    // fan-out plan (host): clip_win = (first window, windows, mode). A window of odd length n is
+    // extracted as n - 1 samples: with an even hop, frames(n) = frames(n - 1) for odd n and no
+    // frame reaches the last sample, so the records are the same and every window starts even
+    std::vector<int64_t> wdesc, xoff(1, 0);
+    std::vector<int32_t> clipwin(3 * (size_t)n_clips);
+    int64_t staged = 0, max_len = 0;
+    for (int c = 0; c < n_clips; ++c) {
+        int64_t lo[3], len[3];
+        int32_t mode = 0;
+        const int nw = aid_exact_windows(offsets[c + 1] - offsets[c], e->cfg.sample_rate, lo, len, &mode);
+        clipwin[3 * c] = (int32_t)(xoff.size() - 1);
+        int used = 0;
+        for (int w = 0; w < nw; ++w) {
+            if (len[w] <= 0) continue;  // the reference sends no query for an empty piece
+            const int64_t m = len[w] & ~(int64_t)1;
+            wdesc.push_back(offsets[c] - offsets[0] + lo[w]);
+            wdesc.push_back(m);
+            wdesc.push_back(staged);
+            staged += m;
+            xoff.push_back(staged);
+            max_len = std::max(max_len, m);
+            ++used;
+        }
+        clipwin[3 * c + 1] = used;
+        clipwin[3 * c + 2] = mode;
+    }
+    const int n_win = (int)(xoff.size() - 1);
+    const float *src = pcm + offsets[0];
+    if (loc == AID_PCM_HOST) {
+        const int64_t n_all = offsets[n_clips] - offsets[0];
+        HIP_TRY(e->x_in.reserve((size_t)std::max<int64_t>(n_all, 1)));
+        if (n_all > 0) HIP_TRY(hipMemcpyAsync(e->x_in.p, src, n_all * sizeof(float), hipMemcpyHostToDevice, s));
+        src = e->x_in.p;
+    }
+    HIP_TRY(e->x_clipwin.reserve(clipwin.size()));
+    HIP_TRY(hipMemcpyAsync(e->x_clipwin.p, clipwin.data(), clipwin.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(e->x_nout.reserve((size_t)n_clips));
+    HIP_TRY(e->x_out.reserve((size_t)n_clips * max_out * 3));
+    std::vector<int32_t> nrows(std::max(n_win, 1), 0);
+    const int mr = e->cfg.max_results;
+    if (n_win > 0) {
+        HIP_TRY(e->x_wdesc.reserve(wdesc.size()));
+        HIP_TRY(hipMemcpyAsync(e->x_wdesc.p, wdesc.data(), wdesc.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(e->x_win.reserve((size_t)std::max<int64_t>(staged, 2)));
+        launch_window_gather(src, e->x_wdesc.p, n_win, max_len, e->x_win.p, s);
+        HIP_TRY(hipGetLastError());
+        if (int rc = extract_locked(e, e->x_win.p, xoff.data(), n_win, AID_PCM_DEVICE, s)) return rc;
+        HIP_TRY(e->q_start.reserve(n_win));
+        HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), n_win * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        if (int rc = run_queries(e, e->records.p, e->q_start.p, e->counts.p, n_win, -1, nullptr, nrows.data(), s))
+            return rc;
+        HIP_TRY(e->q_nrows.reserve((size_t)n_win));
+        HIP_TRY(hipMemcpyAsync(e->q_nrows.p, nrows.data(), n_win * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    } else {
+        HIP_TRY(e->q_nrows.reserve(1));
+        HIP_TRY(e->q_rows.reserve((size_t)mr * 5));
+        HIP_TRY(hipMemsetAsync(e->q_nrows.p, 0, sizeof(int32_t), s));
+    }
+    const double sec = (double)e->cfg.hop / (double)e->cfg.sample_rate;
+    launch_exact_consensus(e->q_rows.p, e->q_nrows.p, mr, e->x_clipwin.p, n_clips, sec, max_out, e->x_out.p, e->x_nout.p,
+                           s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(n_out, e->x_nout.p, (size_t)n_clips * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out, e->x_out.p, (size_t)n_clips * max_out * sizeof(aid_exact_row), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->last_stream = s;
+    return AID_OK;
+}
+

@@ -208,6 +208,27 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
 /* Query with every clip of the last aid_extract (records stay on the device). */
 int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows);
 
+/* Batched exact lane: replaces app/search/exact.py run_exact_lane's
+   sub-window fan-out, the olaf_query calls and the consensus (exact.py:70-124, :132-353) for a
+   batch of clips in one call. Clip c = pcm[offsets[c] .. offsets[c+1]) at the engine's sample
+   rate (the reference's SAMPLE_RATE, exact.py:58). Clips of <= 5 s are queried as the three
+   SUB_WINDOWS (:48-52) and merged by consensus (:220-293), longer clips whole (:296-332);
+   candidates below MIN_ALIGNED_HASHES = 8 are dropped and the rest ranked by confidence
+   min(h/20, 1), stable, descending (:109-121, :340-353). out: host [n_clips][max_out] rows,
+   n_out: host [n_clips]. The metadata lookup (:447-496) stays with the caller. Synchronous. */
+typedef struct aid_exact_row {
+    uint32_t track;          /* engine track id */
+    int32_t aligned_hashes;  /* consensus score */
+    double offset_seconds;   /* median reference_start of the track's rows (binary64, as Python) */
+    double confidence;       /* min(aligned_hashes / 20, 1) */
+} aid_exact_row;
+int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t pcm_location,
+                   int32_t max_out, aid_exact_row *out, int32_t *n_out, void *stream);
+/* The lane's window plan for a clip of n samples (host only, no device): returns the number of
+   windows (3 for clips <= 5 s, mode 1; else 1 whole-clip window, mode 0) with sample bounds
+   lo[w], len[w] (len 0 = no query, as the reference's empty piece, exact.py:150-160, :374-399). */
+int aid_exact_windows(int64_t n, int32_t sample_rate, int64_t *lo, int64_t *len, int32_t *mode);
+
 /* Streaming front end (config 5): interleaved f32 stereo [n_frames][2] -> mono [n_frames] on the
    device, m = (L + R) * 0.5f (the ffmpeg -ac 1 role, decode.py:50-51). Device pointers, stereo
    16-byte and mono 8-byte aligned; asynchronous on `stream`. */
