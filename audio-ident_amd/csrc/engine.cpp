@@ -181,6 +181,7 @@ struct aid_engine {
     int n_clips = 0;
     int64_t total_frames = 0, total_strips = 0, total_chunks = 0, total_records = 0;
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
+    int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     hipStream_t last_stream = nullptr;
     bool have_result = false;
 
@@ -285,6 +286,8 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->cfg = c;
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
+    if (const char *kp = std::getenv("AIDFP_K5_PATH"))
+        e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
     hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
     if (he != hipSuccess) {
         delete e;
@@ -1275,8 +1278,10 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // global histogram: ~2 buckets per expected vote keeps chance buckets >= min_match rare
     int bits = 16;
     while (bits < 24 && (double)(1ull << bits) < 2.0 * votes) ++bits;
-    // LDS fast path only while its 2^16 counters stay sparse (same load bound)
-    const bool fast = 2.0 * votes <= 65536.0;
+    // LDS fast path only while its 2^16 counters stay sparse (same load bound). Heavier
+    // queries are exact on it too (tests/test_gpu_match_load.py) but slower than the global path
+    // (one 16-wave workgroup per CU: 76.7 s against 1.42 s for config 4's 33k windows)
+    const bool fast = e->k5_path == 1 || (e->k5_path == 0 && 2.0 * votes <= 65536.0);
     // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
     // through to the global-histogram path below
     if (fast) {

@@ -280,8 +280,8 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 // Phase 3: the counter region is reused as the exact (track, d) table; only votes whose
 //          bucket is hot are inserted (exact superset filter, as in K5a/K5b).
 // Phase 4: best d per track, rank, write rows (same as K5b). Any table overflow, or a
-//          query too long for 16-bit counters, reports nrows = -1 and the host re-runs it on
-//          the global-histogram path.
+//          16-bit counter reaching 0xFFFF, reports nrows = -1 and the host re-runs the query
+//          on the global-histogram path.
 constexpr int kLdsHistBits = 16;
 constexpr int kFastVoteCap = 4096;
 constexpr int kFastTrackCap = 1024;
@@ -299,6 +299,7 @@ struct FastLds {
     } u;
     uint32_t hot[(1 << kLdsHistBits) / 32];
     int32_t out_n, overflow;
+    uint32_t votes;
 };
 
 __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
@@ -308,13 +309,22 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t mm = (uint32_t)qp.min_match;
     const uint32_t hmask = (1u << kLdsHistBits) - 1;
-    if (n > 30000) {  // 16-bit counters could wrap: let the global path answer
-        if (tid == 0) qp.nrows[q] = -1;
-        return;
-    }
     for (int i = tid; i < (1 << kLdsHistBits) / 2; i += kFastThreads) L.u.hist[i] = 0u;
-    if (tid == 0) { L.out_n = 0; L.overflow = 0; }
+    if (tid == 0) { L.out_n = 0; L.overflow = 0; L.votes = 0; }
     __syncthreads();
+    // total votes (sum of the records' bucket lengths): below 0xFFFF no 16-bit counter can wrap,
+    // so only heavier queries pay for returning atomics (the carry check below)
+    {
+        uint32_t v = 0;
+        for (int64_t i = tid; i < n; i += kFastThreads) {
+            const uint32_t k = key26((uint32_t)qp.recs[a + i]);
+            v += qp.offsets[k + 1] - qp.offsets[k];
+        }
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) atomicAdd(&L.votes, v);
+    }
+    __syncthreads();
+    const bool check_wrap = L.votes >= 0xFFFFu;
     // phase 1
     for (int64_t i = wave; i < n; i += nw) {
         const uint64_t r = qp.recs[a + i];
@@ -326,10 +336,21 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
             const uint32_t tr = (uint32_t)e;
             if (qp.tomb[tr]) continue;
             const uint32_t h = mix_td(tr, (int32_t)(e >> 32) - tq) & hmask;
-            atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
+            if (check_wrap) {
+                const uint32_t old = atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
+                // a 16-bit counter at 0xFFFF would carry into its neighbour: hand the query to
+                // the global path (exactness over speed)
+                if (((old >> (16 * (h & 1))) & 0xFFFFu) == 0xFFFFu) L.overflow = 1;
+            } else {
+                atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
+            }
         }
     }
     __syncthreads();
+    if (L.overflow) {  // uniform: the global path answers this query
+        if (tid == 0) qp.nrows[q] = -1;
+        return;
+    }
     // phase 2
     for (int w = tid; w < (1 << kLdsHistBits) / 32; w += kFastThreads) {
         uint32_t bits = 0;

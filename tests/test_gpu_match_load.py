@@ -1,0 +1,51 @@
+"""K5 under heavy vote load (popular hashes, as a 100k-track catalog has them): rows stay
+identical to the CPU oracle (oracle/fp_match.c, FPSPEC 7) on the LDS fast path (forced, up to
+~10 votes per 16-bit counter; overflows fall back), on the global-histogram path (forced) and
+on the engine's own choice."""
+
+import numpy as np
+import pytest
+
+import oracle as O
+from aidfp import synth
+from aidfp.engine import Engine
+
+pytestmark = pytest.mark.gpu
+SR = 44100
+HOP = 512
+
+
+@pytest.mark.parametrize("path", ["auto", "lds", "global"])
+@pytest.mark.parametrize("per_hash", [0, 30, 90, 160])
+def test_rows_equal_oracle_under_load(per_hash, path, monkeypatch):
+    monkeypatch.setenv("AIDFP_K5_PATH", path)  # read at engine creation
+    rng = np.random.default_rng(per_hash)
+    track = synth.synth(7, 0, 30 * SR, SR)
+    trec = O.fingerprint(track, HOP)
+    queries = [synth.synth(7, s, 5 * SR, SR, snr_db=20.0, salt=3 + i) for i, s in enumerate((SR * 4, SR * 17))]
+    qrecs = [O.fingerprint(q, HOP) for q in queries]
+    h = [(trec & np.uint64(0xFFFFFFFF)).astype(np.uint32)]
+    tr = [np.full(len(trec), 7, np.uint32)]
+    t = [(trec >> np.uint64(32)).astype(np.uint32)]
+    if per_hash:
+        # per_hash postings of random tracks/times for every distinct query hash: chance votes
+        qh = np.unique(np.concatenate([(r & np.uint64(0xFFFFFFFF)).astype(np.uint32) for r in qrecs]))
+        h.append(np.repeat(qh, per_hash))
+        tr.append(rng.integers(1000, 9000, len(qh) * per_hash).astype(np.uint32))
+        t.append(rng.integers(0, 3000, len(qh) * per_hash).astype(np.uint32))
+        # and a few tracks that share a block of the query's hashes at one offset (near-duplicates)
+        for k in range(6):
+            sel = qrecs[0][rng.permutation(len(qrecs[0]))[: 15 + 7 * k]]
+            h.append((sel & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+            tr.append(np.full(len(sel), 20000 + k, np.uint32))
+            t.append(((sel >> np.uint64(32)) + np.uint64(100 + k)).astype(np.uint32))
+    H, TR, T = (np.ascontiguousarray(np.concatenate(a)) for a in (h, tr, t))
+    with Engine(SR) as eng:
+        eng.index_add_postings(H.ctypes.data, TR.ctypes.data, T.ctypes.data, len(H), device=False)
+        eng.index_finalize()
+        post = eng.index_export()
+        got = eng.query(qrecs)
+        for g, r in zip(got, qrecs):
+            ref = O.query(post, r, min_match=eng.min_match, max_rows=eng.max_results)
+            assert np.array_equal(g, ref), (per_hash, g[:4], ref[:4])
+            assert len(g) and g[0, 1] == 7
