@@ -38,13 +38,25 @@ constexpr int kRowsPerStep = 4;
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
 
+// Peak decisions compare powers as int32 keys: a power is >= +0 (never -0: FPSPEC 4's
+// fma(Xr, Xr, Xi*Xi) * 0.25f), and non-negative binary32 values order exactly like their bit
+// patterns. NaN maps to key 0, which reproduces the oracle's `row > l ? row : l` maxima (a NaN
+// neighbour never raises a maximum) and `!(p > thr)` (a NaN is never a peak); +inf keeps its
+// bits. Integer max needs no NaN canonicalisation: hipcc put a `v_max_f32 x, x, x` in front of
+// ~19 of the ~65 fmaxf operands of every row.
+__device__ __forceinline__ int pkey(float x) {
+    const uint32_t b = __float_as_uint(x);
+    return b <= 0x7F800000u ? (int)b : 0;
+}
+
 __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
                                                   uint64_t *__restrict__ mask) {
-    __shared__ __attribute__((aligned(16))) float rows[2][kRowsPerStep][kBins + 32];
+    __shared__ __attribute__((aligned(16))) int rows[2][kRowsPerStep][kBins + 32];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    constexpr int kInf = 0x7F800000;  // key of +inf
 
     // XCD-aware deal: consecutive strips -> blocks b, b+8, b+16 ... (one XCD's L2)
     int64_t strip;
@@ -62,46 +74,48 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
         const int mid = (lo + hi + 1) >> 1;
         if (clips[mid].strip_base <= strip) lo = mid; else hi = mid - 1;
     }
-    const int64_t F = clips[lo].frames;
+    // row indices of one clip fit 32 bits (scalar compares; 64-bit ones went to the VALU)
+    const int F = (int)clips[lo].frames;
     const int64_t fb = clips[lo].frame_base;
-    const int64_t t0 = (strip - clips[lo].strip_base) * strip_len;
-    const int64_t t1 = min(t0 + (int64_t)strip_len, F);
+    const int t0 = (int)(strip - clips[lo].strip_base) * strip_len;
+    const int t1 = min(t0 + strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
+    const int kthr = __float_as_int(thr);                   // thr > 0 (engine config check)
 
     if (tid < 16) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int r = 0; r < kRowsPerStep; ++r) {
-                rows[b][r][tid] = 0.f;
-                rows[b][r][kBins + 16 + tid] = 0.f;
+                rows[b][r][tid] = 0;
+                rows[b][r][kBins + 16 + tid] = 0;
             }
     }
 
     // vertical +-7 as one sliding max: M7(s) = max row-max (fm) over rows s-6..s, built from
     // pair maxima m2[s] = max(fm[s], fm[s-1]) as max(m2[s], m2[s-2], m2[s-4], m2[s-5]).
     // `before` of row s is M7(s-1) (strict), `after` of row s-7 is M7(s) (non-strict).
-    float m2r[8][4];   // pair maxima, slot = iteration & 7
-    float pend[8][4];  // power of this row's candidates (-1 = none), decided 7 rows later
-    float fprev[4], m7p[4];
+    int m2r[8][4];   // pair maxima, slot = iteration & 7
+    int pend[8][4];  // key of this row's candidates (-1 = none), decided 7 rows later
+    int fprev[4], m7p[4];
 #pragma unroll
     for (int s = 0; s < 8; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { m2r[s][i] = 0.f; pend[s][i] = -1.f; }
+        for (int i = 0; i < 4; ++i) { m2r[s][i] = 0; pend[s][i] = -1; }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { fprev[i] = 0.f; m7p[i] = 0.f; }
+    for (int i = 0; i < 4; ++i) { fprev[i] = 0; m7p[i] = 0; }
     // bin 0 is never a peak: its `before` bound is +inf
-    const float kmin_pen = (tid == 0) ? __builtin_huge_valf() : 0.f;
+    const int kmin_pen = (tid == 0) ? kInf : 0;
 
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
-    const int64_t rbeg = t0 - kPeakDT;
-    const int iters = (int)(t1 - t0) + 2 * kPeakDT;
+    const int rbeg = t0 - kPeakDT;
+    const int iters = (t1 - t0) + 2 * kPeakDT;
     float4 pf[AID_K2_PF];  // rows of the next batch(es), in flight
 #pragma unroll
     for (int j = 0; j < AID_K2_PF; ++j) {
-        const int64_t r = rbeg + j;
-        pf[j] = (j < iters && r >= 0 && r < F) ? reinterpret_cast<const float4 *>(P + r * kBins)[tid]
+        const int r = rbeg + j;
+        pf[j] = (j < iters && r >= 0 && r < F) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
                                                : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
@@ -112,71 +126,71 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             if (it >= iters) break;  // workgroup-uniform
             const int buf = (it / kRowsPerStep) & 1;
             if (s % kRowsPerStep == 0) {
-                // stage rows it .. it+3, then fetch rows it+4 .. it+7 (register staging beats
+                // stage rows it .. it+3 as keys, then fetch rows it+PF .. (register staging beats
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll
                 for (int j = 0; j < kRowsPerStep; ++j) {
                     const int slot = (s + j) % AID_K2_PF;  // compile-time: the loop is unrolled by 8
-                    reinterpret_cast<float4 *>(&rows[buf][j][16])[tid] = pf[slot];
-                    const int64_t rn = rbeg + it + j + AID_K2_PF;
+                    const float4 v = pf[slot];
+                    reinterpret_cast<int4 *>(&rows[buf][j][16])[tid] = make_int4(pkey(v.x), pkey(v.y), pkey(v.z), pkey(v.w));
+                    const int rn = rbeg + it + j + AID_K2_PF;
                     pf[slot] = (it + j + AID_K2_PF < iters && rn >= 0 && rn < F)
-                                   ? reinterpret_cast<const float4 *>(P + rn * kBins)[tid]
+                                   ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
                 __syncthreads();
             }
-            const int64_t r = rbeg + it;
-            const float *rb = rows[buf][s % kRowsPerStep];
-            float q[36];  // bins 4j-16 .. 4j+19 (zero outside the frame)
+            const int r = rbeg + it;
+            const int *rb = rows[buf][s % kRowsPerStep];
+            int q[36];  // bins 4j-16 .. 4j+19 (zero outside the frame)
 #pragma unroll
             for (int v = 0; v < 9; ++v) {
-                const float4 w = reinterpret_cast<const float4 *>(rb)[tid + v];
+                const int4 w = reinterpret_cast<const int4 *>(rb)[tid + v];
                 q[4 * v + 0] = w.x; q[4 * v + 1] = w.y; q[4 * v + 2] = w.z; q[4 * v + 3] = w.w;
             }
-            // keep the two unused edge floats live: otherwise hipcc re-pairs the used floats into
+            // keep the two unused edge values live: otherwise hipcc re-pairs the used ones into
             // ds_read2_b32 at a 16-byte lane stride (8-way bank conflict) instead of 9 ds_read_b128
             asm volatile("" ::"v"(q[0]), "v"(q[35]));
             // own bin i is q[16+i]; left window q[1+i..15+i], right window q[17+i..31+i]
-            float midL = q[4], midR = q[20];
+            int midL = q[4], midR = q[20];
 #pragma unroll
-            for (int u = 5; u <= 15; ++u) midL = fmaxf(midL, q[u]);
+            for (int u = 5; u <= 15; ++u) midL = max(midL, q[u]);
 #pragma unroll
-            for (int u = 21; u <= 31; ++u) midR = fmaxf(midR, q[u]);
-            float L[4], R[4];
-            L[0] = fmaxf(fmaxf(q[1], q[2]), fmaxf(q[3], midL));
-            L[1] = fmaxf(fmaxf(q[2], q[3]), fmaxf(midL, q[16]));
-            L[2] = fmaxf(fmaxf(q[3], midL), fmaxf(q[16], q[17]));
-            L[3] = fmaxf(fmaxf(midL, q[16]), fmaxf(q[17], q[18]));
-            R[0] = fmaxf(fmaxf(q[17], q[18]), fmaxf(q[19], midR));
-            R[1] = fmaxf(fmaxf(q[18], q[19]), fmaxf(midR, q[32]));
-            R[2] = fmaxf(fmaxf(q[19], midR), fmaxf(q[32], q[33]));
-            R[3] = fmaxf(fmaxf(midR, q[32]), fmaxf(q[33], q[34]));
+            for (int u = 21; u <= 31; ++u) midR = max(midR, q[u]);
+            int L[4], R[4];
+            L[0] = max(max(q[1], q[2]), max(q[3], midL));
+            L[1] = max(max(q[2], q[3]), max(midL, q[16]));
+            L[2] = max(max(q[3], midL), max(q[16], q[17]));
+            L[3] = max(max(midL, q[16]), max(q[17], q[18]));
+            R[0] = max(max(q[17], q[18]), max(q[19], midR));
+            R[1] = max(max(q[18], q[19]), max(midR, q[32]));
+            R[2] = max(max(q[19], midR), max(q[32], q[33]));
+            R[3] = max(max(midR, q[32]), max(q[33], q[34]));
 
-            // candidates only inside the strip's output rows (uniform)
-            // (rows outside get threshold +inf)
-            const float thr_row = (r >= t0 && r < t1) ? thr : __builtin_huge_valf();
+            // candidates only inside the strip's output rows (uniform): other rows get +inf
+            const int thr_row = (r >= t0 && r < t1) ? kthr : kInf;
             bool pk[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float p = q[16 + i];
-                const float fm = fmaxf(fmaxf(L[i], p), R[i]);
-                const float m2 = fmaxf(fm, fprev[i]);
+                const int p = q[16 + i];
+                const int fm = max(max(L[i], p), R[i]);
+                const int m2 = max(fm, fprev[i]);
                 fprev[i] = fm;
                 m2r[s][i] = m2;
-                const float m7 = fmaxf(fmaxf(fmaxf(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
-                const float bf = fmaxf(fmaxf(i == 0 ? fmaxf(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
+                const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
+                const int bf = max(max(i == 0 ? max(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
                 m7p[i] = m7;
-                // candidate: p > before (strict) and p >= right window; power >= 0, so -1 = none
-                const float c1 = (p > bf) ? p : -1.f;
+                // candidate: p > before (strict) and p >= right window; keys >= 0, so -1 = none
+                const int c1 = (p > bf) ? p : -1;
                 // row r-7 (slot s+1) has now met all 7 later rows: p >= their row-max
                 pk[i] = pend[(s + 1) & 7][i] >= m7;
-                pend[s][i] = (c1 >= R[i]) ? c1 : -1.f;
+                pend[s][i] = (c1 >= R[i]) ? c1 : -1;
             }
             const uint64_t b0 = __ballot(pk[0]), b1 = __ballot(pk[1]), b2 = __ballot(pk[2]), b3 = __ballot(pk[3]);
-            const int64_t rd = r - kPeakDT;
+            const int rd = r - kPeakDT;
             if (rd >= t0 && rd < t1 && lane < 4) {
                 const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-                M[rd * kMaskWords] = wv;
+                M[(int64_t)rd * kMaskWords] = wv;
             }
         }
     }

@@ -167,3 +167,23 @@ def test_max_duration_clip(gpu_engine):
         assert len(got[c]) == len(r), c
         assert np.array_equal(got[c], r), c
     assert len(got[1]) > 100000
+
+
+def test_nonfinite_huge_and_tied_inputs(gpu_engine):
+    """K2 compares powers as int32 keys (NaN -> 0): NaN/inf PCM (NaN and inf powers), powers that
+    overflow to inf, and exactly tied powers give the oracle's peaks and hashes bit for bit."""
+    rng = np.random.default_rng(3)
+    a = _clip(41, 200000, snr=20)
+    a[[5000, 70000, 150001]] = [np.nan, np.inf, -np.inf]
+    b = _clip(42, 120000) * np.float32(3e18)  # squares overflow binary32: inf powers next to finite
+    c = np.zeros(150000, np.float32)  # a repeating integer-exact pattern: tied powers across frames
+    c[::512] = 8.0
+    c[256::1024] = -4.0
+    d = (rng.integers(-3, 4, 180000) / 4).astype(np.float32)  # coarse values, many equal powers
+    clips = [a, b, c, d]
+    got = gpu_engine.extract_host(clips)
+    for i, x in enumerate(clips):
+        ref_pk = O.peaks(O.stft_power(x, HOP))
+        pk = peaks_from_mask(gpu_engine.peakmask(i, len(x)))
+        assert np.array_equal(pk, ref_pk.reshape(-1, 2)), f"clip {i}: peaks differ"
+        assert np.array_equal(got[i], O.fingerprint(x, HOP)), f"clip {i}: hashes differ"
