@@ -22,8 +22,9 @@
 #include "resample_design.h"
 
 namespace aid {
-void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_strips, int hop,
-                       const Tables *tab, float *out, bool logmag, hipStream_t s);
+void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
+                       int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
+                       hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
                       uint64_t *mask, hipStream_t s);
@@ -181,6 +182,7 @@ struct aid_engine {
     int n_clips = 0;
     int64_t total_frames = 0, total_strips = 0, total_chunks = 0, total_records = 0;
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
+    int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
     int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     hipStream_t last_stream = nullptr;
     bool have_result = false;
@@ -286,6 +288,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->cfg = c;
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
+    e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
     hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
@@ -501,7 +504,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     if (frames > 0) {
         {
             ProfScope ps(e, AID_K_STFT, s);
-            launch_stft_power(dpcm, e->desc.p, n_clips, kstrips, hop, e->d_tab, e->power.p, false, s);
+            launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false, s);
         }
         if (loc == AID_PCM_HOST) {
             if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
@@ -620,7 +623,8 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_pcm, pcm, n * sizeof(float), hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
-        launch_stft_power(d_pcm, d_desc, 1, (F + kStftStrip - 1) / kStftStrip, e->cfg.hop, e->d_tab, d_out, true, s);
+        launch_stft_power(d_pcm, d_desc, 1, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
+                          d_out, true, s);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);

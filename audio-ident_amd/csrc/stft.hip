@@ -39,6 +39,11 @@
 #ifndef AID_K1_WINREG
 #define AID_K1_WINREG 0
 #endif
+// AID_K1_BALANCED=1 (default): waves take equal frame ranges of the whole batch (ring restarts
+// only at clip edges) instead of 16-frame strips; 0 = strips (A/B)
+#ifndef AID_K1_BALANCED
+#define AID_K1_BALANCED 1
+#endif
 // AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
 // (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
 
@@ -53,8 +58,8 @@ __device__ __forceinline__ int e3(int k) { return k ^ (((k >> 4) & 3) << 2); }
 template <bool LOGMAG, int ROWS>
 __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
-                                                                int64_t total_strips, const Tables *__restrict__ tab,
-                                                                float *__restrict__ out) {
+                                                                int64_t total, int64_t n_waves,
+                                                                const Tables *__restrict__ tab, float *__restrict__ out) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
@@ -65,7 +70,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     __shared__ float4 s_win4[512], s_ta4[512], s_t2p[512];
     __shared__ float4 s_tb4[32];  // [h][lane & 3]: T64[m2*j1] depends on the lane only through m2
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar strip/segment math
     float2 *buf = lds[wave];
     const int kq = lane >> 2;  // stage B/C: k1
     const int mq = lane & 3;   // stage B: m2 ; stage C: s
@@ -98,8 +103,24 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     for (int i = 0; i < 10; ++i) t16[i] = tab->t16[i];
     __syncthreads();
 
+#if AID_K1_BALANCED
+    // wave g takes frames [g*T/W, (g+1)*T/W) of the batch's T frames (W waves): every wave has
+    // the same work (no partial last round), and a segment restarts the ring only at a clip edge
+    const int64_t g = (int64_t)blockIdx.x * kStftWaves + wave;
+    if (g >= n_waves) return;  // wave-uniform, after the only barrier
+    int64_t f = g * total / n_waves;
+    const int64_t f_end = (g + 1) * total / n_waves;
+    while (f < f_end) {
+    int lo = 0, hi = n_clips - 1;
+    while (lo < hi) {  // last clip with frame_base <= f (scalar loads): the clip holding frame f
+        const int mid = (lo + hi + 1) >> 1;
+        if (clips[mid].frame_base <= f) lo = mid; else hi = mid - 1;
+    }
+    const int64_t t0 = f - clips[lo].frame_base;
+    const int nfr = (int)min(f_end - f, clips[lo].frames - t0);
+#else
     const int64_t strip = (int64_t)blockIdx.x * kStftWaves + wave;
-    if (strip >= total_strips) return;  // wave-uniform, after the only barrier
+    if (strip >= total) return;  // wave-uniform, after the only barrier
     int lo = 0, hi = n_clips - 1;
     while (lo < hi) {  // last clip with stft_base <= strip (scalar loads)
         const int mid = (lo + hi + 1) >> 1;
@@ -107,6 +128,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     }
     const int64_t t0 = (strip - clips[lo].stft_base) * kStftStrip;
     const int nfr = (int)min((int64_t)kStftStrip, clips[lo].frames - t0);
+#endif
     const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + lane;
     float *dst = out + (clips[lo].frame_base + t0) * kBins;
 
@@ -244,26 +266,41 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
             }
         }
     }
+#if AID_K1_BALANCED
+    f += nfr;
+    }
+#endif
 }
 
 template <bool LOGMAG>
 static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
-                        int64_t total_strips, const Tables *tab, float *out) {
+                        int64_t total, int64_t n_waves, const Tables *tab, float *out) {
     switch (rows) {
-        case 1: hipLaunchKernelGGL((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
-        case 2: hipLaunchKernelGGL((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
-        case 4: hipLaunchKernelGGL((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
-        case 8: hipLaunchKernelGGL((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
-        default: hipLaunchKernelGGL((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total_strips, tab, out); break;
+        case 1: hipLaunchKernelGGL((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
+        case 2: hipLaunchKernelGGL((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
+        case 4: hipLaunchKernelGGL((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
+        case 8: hipLaunchKernelGGL((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
+        default: hipLaunchKernelGGL((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
     }
 }
 
-void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_strips, int hop,
-                       const Tables *tab, float *out, bool logmag, hipStream_t s) {
-    if (total_strips <= 0) return;
-    const dim3 g((unsigned)((total_strips + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
-    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total_strips, tab, out);
-    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total_strips, tab, out);
+// total_frames = sum of the clips' frames, total_strips = sum of ceil(F / kStftStrip) (strip mode),
+// slots = resident K1 waves on the device (CUs x kStftWaves)
+void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
+                       int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
+                       hipStream_t s) {
+    if (total_frames <= 0) return;
+#if AID_K1_BALANCED
+    // one round of equal ranges; at least kStftStrip frames per wave (a ring fill per segment)
+    const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>(slots, total_frames / kStftStrip));
+    const int64_t total = total_frames;
+#else
+    const int64_t n_waves = total_strips, total = total_strips;
+    (void)slots;
+#endif
+    const dim3 g((unsigned)((n_waves + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
+    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out);
+    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out);
 }
 
 }  // namespace aid
