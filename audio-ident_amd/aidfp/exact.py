@@ -126,11 +126,12 @@ async def _default_query(pcm: bytes) -> list[OlafMatch]:
     return await olaf_query(pcm)
 
 
-async def _query_subwindows(pcm: bytes, duration: float, query: QueryFn) -> list[ScoredCandidate]:
+async def _query_subwindows(pcm: bytes, duration: float, query: QueryFn,
+                            sample_rate: int = SAMPLE_RATE) -> list[ScoredCandidate]:
     per_window: list[list[OlafMatch]] = []
     for a, b in SUB_WINDOWS:
         stop = min(b, duration)
-        piece = extract_pcm_window(pcm, a, stop) if a < stop else b""
+        piece = extract_pcm_window(pcm, a, stop, sample_rate) if a < stop else b""
         if not piece:
             per_window.append([])
             continue
@@ -173,7 +174,7 @@ async def enrich(top: list[ScoredCandidate], lookup: LookupFn) -> list[ExactMatc
 
 
 async def run_exact_lane(pcm_16k: bytes, max_results: int = 10, *, query: QueryFn | None = None,
-                         lookup: LookupFn | None = None) -> list[ExactMatch]:
+                         lookup: LookupFn | None = None, sample_rate: int = SAMPLE_RATE) -> list[ExactMatch]:
     """Reference semantics of run_exact_lane (exact.py:70-124) over the GPU engine.
 
     With the default query function the whole lane (fan-out, match, consensus, ranking) is one
@@ -182,9 +183,9 @@ async def run_exact_lane(pcm_16k: bytes, max_results: int = 10, *, query: QueryF
         return []
     if query is None:
         return (await run_exact_lane_batch([pcm_16k], max_results, lookup=lookup))[0]
-    duration = pcm_duration_sec(pcm_16k)
+    duration = pcm_duration_sec(pcm_16k, sample_rate)  # sample_rate: the reference's SAMPLE_RATE (16 kHz)
     if duration <= SHORT_CLIP_THRESHOLD_SEC:
-        scored = await _query_subwindows(pcm_16k, duration, query)
+        scored = await _query_subwindows(pcm_16k, duration, query, sample_rate)
     else:
         scored = await _query_full(pcm_16k, query)
     return await enrich(rank(scored, max_results), lookup or _default_lookup)

@@ -116,3 +116,37 @@ def test_single_clip_default_path(service):
         fp.set_service(None)
     assert res and res[0].track == IDS[6] and res[0].confidence == 1.0
     assert abs(res[0].offset_seconds - 12.75) < 0.5
+
+
+def test_lane_at_44k_odd_windows():
+    """At 44.1 kHz the 0.75 s sub-window starts at an odd sample (33075) and windows can have odd
+    lengths: the lane stages them even and extracts n - 1 samples of an odd window (same frames
+    for an even hop). Rows must equal the per-window path on the engine's own queries."""
+    sr = 44100
+    eng = Engine(sr, device=0, min_match=5)
+    try:
+        tracks = np.arange(12, dtype=np.uint32) + 300
+        for t in tracks:
+            eng.index_add_records(int(t), eng.extract_host([synth.synth(int(t), 0, 20 * sr, sr)])[0])
+        eng.index_finalize()
+        cs = [synth.synth(int(tracks[i % 12]), sr * (i + 1) + 7 * i, n, sr, snr_db=20, salt=i)
+              for i, n in enumerate([5 * sr, 5 * sr - 1, 4 * sr + 3, int(3.3 * sr) + 1, 2 * sr + 1, 6 * sr + 1,
+                                     sr // 3, 5 * sr + 2])]
+        names = {int(t): str(uuid.UUID(int=int(t))) for t in tracks}
+        sec = eng.hop / eng.sample_rate
+
+        async def query(piece):
+            x = np.frombuffer(piece, dtype="<f4")
+            eng.extract_host([x])
+            rows = eng.query_extracted()[0]
+            return [fp.OlafMatch(int(c), q0 * sec, q1 * sec, names[int(t)], int(t), (q0 + d) * sec, (q1 + d) * sec)
+                    for c, t, d, q0, q1 in rows.tolist()]
+
+        lane = eng.exact_lane(cs)
+        for i, x in enumerate(cs):
+            want = asyncio.run(ex.run_exact_lane(x.astype("<f4").tobytes(), 10, query=query, sample_rate=sr))
+            got = ex.candidates_from_rows(lane[i], names, 10)
+            assert [(c.track_uuid, c.aligned_hashes, c.offset_seconds, c.confidence) for c in got] == \
+                   [(m.track, m.aligned_hashes, m.offset_seconds, m.confidence) for m in want], i
+    finally:
+        eng.close()
