@@ -6,18 +6,19 @@
 // :185-193 query).
 //
 // Work mapping (gfx950, wave64):
-//   * each wave owns a strip of kStftStrip consecutive frames of one clip. Lane l
+//   * each wave owns an equal range of the batch's frames (AID_K1_BALANCED). Lane l
 //     keeps the complex samples z[64*n1 + l] (n1 < 16, "rows" of 128 PCM samples)
 //     in a 16-slot register ring: frame t+1 reuses 16 - H/128 rows of frame t, so
 //     only the new hop is loaded (H/128 float2 loads per lane, 512 contiguous bytes
-//     per wave-instruction) and every PCM byte crosses HBM -> VGPR once per strip;
+//     per wave-instruction) and every PCM byte crosses HBM -> VGPR once per range (the ring
+//     restarts at clip edges only);
 //     the next frame's rows are loaded right after the window multiply so their
 //     latency hides under the FFT;
 //   * stage A = 16-point DFT in registers, twiddle (LDS table laid out [k1][lane]),
 //     LDS transpose (E1, row stride 68 float2: conflict-free write and read);
-//   * stage B = 16-point DFT in registers, twiddle, quad exchange through LDS
-//     (E2, lane stride 17 float2);
-//   * stage C = radix-4 in registers, spill to LDS in XOR-swizzled natural order
+//   * stage B = 16-point DFT in registers, twiddle;
+//   * stage C = radix-4 across the lane quad with DPP (AID_K1_DPPC; formerly a quad exchange
+//     E2 through LDS + radix-4 in registers), spill to LDS in XOR-swizzled natural order
 //     (E3), then the real split reads each mirror pair (Z[k], Z[1024-k]) once
 //     (conflict-free) and produces both bins; stores are 64 consecutive bins per
 //     wave-instruction (the mirror bins in descending order, same 256-B segment).
@@ -44,6 +45,15 @@
 #ifndef AID_K1_BALANCED
 #define AID_K1_BALANCED 1
 #endif
+// AID_K1_DPPC: stage C's DFT4 over m2 runs across the lane quad with DPP operands (two
+// butterflies of fma(partner, +-1, self) and a -i rotation in lane 3) instead of the E2 quad
+// exchange through LDS; the results then sit at Z[kq + 16*j1 + 256*bitrev2(mq)] and E3 uses the
+// swizzle "bit 4 ^= bit 9". 2 (default) = hand-placed v_fmac_f32_dpp (K1 0.386 -> 0.377 ms in
+// same-box A/Bs), 1 = the same arithmetic through intrinsics (hipcc keeps a separate
+// v_mov_b32_dpp per operand: 0.393), 0 = E2 through LDS
+#ifndef AID_K1_DPPC
+#define AID_K1_DPPC 2
+#endif
 // AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
 // (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
 
@@ -53,7 +63,19 @@ namespace aid {
 // group hold k = kq + 16*mq (+const): k ^ (mq << 2) puts them on 16 distinct 8-byte bank
 // pairs; the readers (k = lane + 64i, and the mirror 1024-k) stay a permutation of one or two
 // 16-entry blocks, so every access is conflict-free (the mirror read: one 2-way pair per wave).
+#if AID_K1_DPPC
+// E3 slot of Z[k] (DPP stage C): bit 4 ^= bit 9. Writers (k = kq + 16 j1 + 256 j2, one j1 per
+// instruction) then hit 32 distinct 8-byte bank pairs twice each; the real split reads Z[k] for
+// k < 512 unswizzled and the mirrors (>= 512) with bit 4 flipped, both conflict-free.
+__device__ __forceinline__ int e3(int k) { return k ^ (((k >> 9) & 1) << 4); }
+// partner value across the lane quad (DPP quad_perm; every lane of the quad is valid)
+template <int CTRL>
+__device__ __forceinline__ float quad_dpp(float x) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+#else
 __device__ __forceinline__ int e3(int k) { return k ^ (((k >> 4) & 3) << 2); }
+#endif
 
 template <bool LOGMAG, int ROWS>
 __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
@@ -79,9 +101,20 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     //   Z[lane + 64i]: bits 4-5 are those of lane                              -> e3a + 64i
     //   Z[1024 - lane - 64i] = Z[64(15-i) + m], m = 64 - lane in 1..64         -> e3b + 64(15-i)
     //   (except k = 0, whose mirror is Z[0] itself)
+#if AID_K1_DPPC
+    // writer slots: e3(kq + 16 j1 + 256 j2) = kq + 256 j2 + 16 (j1 ^ (j2 >> 1)) = base[j1 & 1] + 16 j1
+    const int j2q = ((mq & 1) << 1) | (mq >> 1);  // lane mq holds output j2 = bitrev2(mq)
+    const int e3w0 = kq + 256 * j2q + 16 * (j2q >> 1), e3w1 = kq + 256 * j2q - 16 * (j2q >> 1);
+    const int e3a = lane;                            // Z[lane + 64 i], i < 8: bit 9 clear
+    const int e3b = (lane == 0) ? 80 : ((64 - lane) ^ 16);  // Z[64 (15 - i) + 64 - lane] ^ 16
+    const float s1 = mq < 2 ? 1.0f : -1.0f;                     // butterfly over lanes (mq, mq ^ 2)
+    const float s2 = (mq == 1 || mq == 2) ? -1.0f : 1.0f;       // butterfly over lanes (mq, mq ^ 1)
+    const float s0 = lane == 0 ? 1.0f : -1.0f;  // sign of Z[0]'s mirror slot for i = 0 (Z[0] itself)
+#else
     const int e3w = (kq ^ (mq << 2)) + 16 * mq;
     const int e3a = e3(lane);
     const int e3b = e3(64 - lane);
+#endif
 
     for (int i = threadIdx.x; i < 512; i += kStftWaves * 64) {
         const int h = i >> 6, l = i & 63, a = 2 * h, b = 2 * h + 1;
@@ -194,6 +227,70 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
                     v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
                 }
+#if AID_K1_DPPC
+                // stage C across the quad (FPSPEC 3 DFT4 over m2 = mq, for every j1), each butterfly
+                // one in-place fma with the partner as DPP operand: x <- partner * s + x
+                //   s1 = (+1, +1, -1, -1): lanes 0..3 -> t0, t2, -t1, -t3
+                //   lane 3: u = -i t3 from -t3: (-T.im, T.re); lanes 0..2 keep their value
+                //   s2 = (+1, -1, -1, +1): lanes 0..3 -> y0, -y2, -y1, -y3
+                // fma(p, +-1, x) rounds x +- p once: FPSPEC's add/sub values; the signs are exact
+                // and cancel in the real split (see there)
+#if AID_K1_DPPC == 2
+                // hand-placed: v_fmac_f32_dpp (partner * s + x, in place) keeps the DPP inside the
+                // fma; the leading s_nop 1 covers the VALU-write -> DPP-read hazard of the block's
+                // inputs, and every other DPP source was written >= 2 instructions earlier
+#pragma unroll
+                for (int j0 = 0; j0 < 16; j0 += 4) {
+                    float u0, w0, u1, w1, u2, w2, u3, w3;
+                    asm volatile(
+                        "s_nop 1\n\t"
+                        "v_fmac_f32_dpp %8, %8, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %9, %9, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %10, %10, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %11, %11, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %12, %12, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %13, %13, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %14, %14, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %15, %15, %16 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_cndmask_b32_e64 %0, %8, -%9, %18\n\t"
+                        "v_cndmask_b32_e64 %1, %9, %8, %18\n\t"
+                        "v_cndmask_b32_e64 %2, %10, -%11, %18\n\t"
+                        "v_cndmask_b32_e64 %3, %11, %10, %18\n\t"
+                        "v_cndmask_b32_e64 %4, %12, -%13, %18\n\t"
+                        "v_cndmask_b32_e64 %5, %13, %12, %18\n\t"
+                        "v_cndmask_b32_e64 %6, %14, -%15, %18\n\t"
+                        "v_cndmask_b32_e64 %7, %15, %14, %18\n\t"
+                        "v_fmac_f32_dpp %0, %0, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %1, %1, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %2, %2, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %3, %3, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %4, %4, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %5, %5, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %6, %6, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                        "v_fmac_f32_dpp %7, %7, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+                        : "=&v"(u0), "=&v"(w0), "=&v"(u1), "=&v"(w1), "=&v"(u2), "=&v"(w2), "=&v"(u3), "=&v"(w3),
+                          "+v"(v[j0].x), "+v"(v[j0].y), "+v"(v[j0 + 1].x), "+v"(v[j0 + 1].y), "+v"(v[j0 + 2].x),
+                          "+v"(v[j0 + 2].y), "+v"(v[j0 + 3].x), "+v"(v[j0 + 3].y)
+                        : "v"(s1), "v"(s2), "s"(0x8888888888888888ull));
+                    v[j0] = make_float2(u0, w0);
+                    v[j0 + 1] = make_float2(u1, w1);
+                    v[j0 + 2] = make_float2(u2, w2);
+                    v[j0 + 3] = make_float2(u3, w3);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) buf[(((j0 + j) & 1) ? e3w1 : e3w0) + 16 * (j0 + j)] = v[j0 + j];
+                }
+#else
+#pragma unroll
+                for (int j1 = 0; j1 < 16; ++j1) {
+                    float2 x = v[j1];
+                    x.x = __builtin_fmaf(quad_dpp<0x4E>(x.x), s1, x.x);
+                    x.y = __builtin_fmaf(quad_dpp<0x4E>(x.y), s1, x.y);
+                    const float ux = mq == 3 ? -x.y : x.x, uy = mq == 3 ? x.x : x.y;
+                    v[j1] = make_float2(__builtin_fmaf(quad_dpp<0xB1>(ux), s2, ux), __builtin_fmaf(quad_dpp<0xB1>(uy), s2, uy));
+                    buf[((j1 & 1) ? e3w1 : e3w0) + 16 * j1] = v[j1];
+                }
+#endif
+#else
                 // E2: lane (kq, m2) writes B[kq][m2][j1]; reader lane (kq, s = mq) takes j1 = s + 4r
                 if (AID_K1_DIAG != 7) {
 #pragma unroll
@@ -219,6 +316,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         if (AID_K1_DIAG != 8) buf[a] = v[4 * r + j2];
                     }
                 }
+#endif
                 wave_lds_sync();
                 float *drow = dst + (int64_t)f * kBins;
                 float acc10 = 0.f;
@@ -231,7 +329,15 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[e3a + 64 * i];
                     // k = 0 mirrors onto itself (Z[0]): lane 0's e3b + 960 would be slot 1024
                     const int bi = (i == 0 && lane == 0) ? 0 : e3b + 64 * (15 - i);
+#if AID_K1_DPPC
+                    // stored Z[k] is -Z[k] for k >= 256 (lanes 1..3 of stage C): for i < 4, a is exact
+                    // and b is stored negated (except Z[0] for lane 0, i = 0), so flip b; for i >= 4 both
+                    // are negated, every sum below flips sign and the squares in P do not see it
+                    const float2 bs = buf[bi];
+                    const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
+#else
                     const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[AID_K1_DIAG == 2 ? e3(k ^ 512) : bi];
+#endif
                     const float er = a.x + b.x, ei = a.y - b.y;
                     const float orr = a.y + b.y, oi = b.x - a.x;
                     const float4 t2 = s_t2p[64 * i + lane];
