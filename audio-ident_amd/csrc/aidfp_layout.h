@@ -13,14 +13,16 @@ constexpr int kZoneDF = 127;      // target zone, bins
 constexpr int kFan = 10;          // targets per anchor
 constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 
-// K1: kStftWaves waves per workgroup (14: +2 % over 12 in same-box A/Bs), each wave slides over a strip of kStftStrip frames
+// K1: kStftWaves waves per workgroup, one workgroup per CU. With stage C on DPP (no E2) the
+// exchange buffer is an unpadded, XOR-swizzled 8 KB per wave, so 16 waves (4 per SIMD at
+// <= 128 VGPRs) + 24.5 KB of tables fit the 160 KB LDS: K1 0.383 -> 0.366 ms over 14 padded waves
 #ifndef AID_STFT_WAVES
-#define AID_STFT_WAVES 14  // 14 x 8.5 KB exchange buffers + 32 KB tables fit the 160 KB LDS; VGPRs capped at 128
+#define AID_STFT_WAVES 16
 #endif
 constexpr int kStftWaves = AID_STFT_WAVES;
 constexpr int kStftStrip = 16;
 #ifndef AID_K1_COMPACT
-#define AID_K1_COMPACT 0
+#define AID_K1_COMPACT 1
 #endif
 constexpr int kStftLdsPerWave = AID_K1_COMPACT ? 1024 : 1088;  // float2 entries (E1: 16x68, E2: 64x17, E3: 1024)
 
