@@ -19,21 +19,27 @@
 // clip's record count.
 #include "aidfp_device.h"
 
+#ifndef AID_K3_THREADS
+#define AID_K3_THREADS 512  // 256: 0.055 ms, 512: 0.040, 1024: 0.040 (one workgroup per clip at 256 x 10 s)
+#endif
+
 namespace aid {
 
-__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[256+1]*/, int64_t *total) {
+constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
+
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK3]*/, int64_t *total) {
     const int tid = threadIdx.x;
     tmp[tid] = v;
     __syncthreads();
-    // Hillis-Steele over 256 entries (small; runs once per phase)
-    for (int off = 1; off < 256; off <<= 1) {
+    // Hillis-Steele over kK3 entries (small; runs once per phase)
+    for (int off = 1; off < kK3; off <<= 1) {
         const int64_t add = tid >= off ? tmp[tid - off] : 0;
         __syncthreads();
         tmp[tid] += add;
         __syncthreads();
     }
     const int64_t incl = tmp[tid];
-    if (total) *total = tmp[255];
+    if (total) *total = tmp[kK3 - 1];
     __syncthreads();
     return incl - v;
 }
@@ -61,12 +67,12 @@ __device__ __forceinline__ uint32_t make_hash(int k1, int k2, int dt) {
 }
 
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ mask, const ClipDesc *__restrict__ clips,
+__global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ mask, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_chunks, int64_t *__restrict__ chunk_counts,
                                                   uint64_t *__restrict__ records, int64_t *__restrict__ clip_counts) {
     __shared__ uint32_t plist[kHashChunkPeakCap];
     __shared__ uint32_t foff[kHashChunk + kZoneDT + 2];
-    __shared__ int64_t scan_tmp[256];
+    __shared__ int64_t scan_tmp[kK3];
     const int tid = threadIdx.x;
     const int64_t chunk = blockIdx.x;
     if (chunk >= total_chunks) return;
@@ -87,7 +93,7 @@ __global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ 
     if (!WRITE && nck == 1) return;  // single-chunk clips: the WRITE pass needs no base
 
     // 1. per-frame counts over a contiguous run of frames per thread, block scan
-    const int per = (nf + 255) / 256;
+    const int per = (nf + kK3 - 1) / kK3;
     const int fa = min(tid * per, nf), fz = min(fa + per, nf);
     int64_t mine = 0;
     for (int f = fa; f < fz; ++f) {
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ 
     const int n_anchor = (int)foff[c1 - c0];
 
     // 3. anchors: contiguous run per thread
-    const int pa_per = (n_anchor + 255) / 256;
+    const int pa_per = (n_anchor + kK3 - 1) / kK3;
     const int aa = min(tid * pa_per, n_anchor), az = min(aa + pa_per, n_anchor);
     int64_t my = 0;
     for (int i = aa; i < az; ++i) {
@@ -151,11 +157,11 @@ __global__ __launch_bounds__(256) void k_landmarks(const uint64_t *__restrict__ 
         } else {
             // base of this chunk inside the clip = sum of the clip's earlier chunks
             int64_t pre = 0;
-            for (int64_t c = cd.chunk_base + tid; c < chunk; c += 256) pre += chunk_counts[c];
+            for (int64_t c = cd.chunk_base + tid; c < chunk; c += kK3) pre += chunk_counts[c];
             block_excl_scan(pre, scan_tmp, &before);
             if (q == 0) {
                 int64_t all = 0;
-                for (int64_t c = cd.chunk_base + tid; c < cd.chunk_base + nck; c += 256) all += chunk_counts[c];
+                for (int64_t c = cd.chunk_base + tid; c < cd.chunk_base + nck; c += kK3) all += chunk_counts[c];
                 int64_t tot = 0;
                 block_excl_scan(all, scan_tmp, &tot);
                 if (tid == 0) clip_counts[lo] = tot;
@@ -187,10 +193,10 @@ void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, 
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s) {
     if (total_chunks <= 0) return;
     if (write)
-        hipLaunchKernelGGL(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(256), 0, s, mask, clips, n_clips,
+        hipLaunchKernelGGL(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
                            total_chunks, chunk_counts, records, clip_counts);
     else
-        hipLaunchKernelGGL(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(256), 0, s, mask, clips, n_clips,
+        hipLaunchKernelGGL(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
                            total_chunks, chunk_counts, records, clip_counts);
 }
 
