@@ -55,7 +55,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
-                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, hipStream_t s);
+                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s);
 uint32_t index_keys();
 void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
 void launch_window_gather(const float *src, const int64_t *win, int n_win, int64_t max_len, float *dst, hipStream_t s);
@@ -184,6 +184,7 @@ struct aid_engine {
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
     int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
+    int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     hipStream_t last_stream = nullptr;
     bool have_result = false;
 
@@ -1024,6 +1025,7 @@ int aid_index_remove(aid_engine *e, uint32_t track) {
     if (track >= e->n_tracks || e->h_tomb[track]) return fail(AID_ERR_INVALID, "track not indexed");
     HIP_TRY(hipSetDevice(e->device));
     e->h_tomb[track] = 1;
+    ++e->tomb_since_build;  // the CSR still holds its postings until the next finalize
     HIP_TRY(hipMemcpy(e->tomb.p + track, &e->h_tomb[track], 1, hipMemcpyHostToDevice));
     return AID_OK;
 }
@@ -1058,6 +1060,7 @@ static int finalize_locked(aid_engine *e) {
     e->n_indexed = total;
     e->index_built = true;
     e->index_dirty = false;
+    e->tomb_since_build = 0;  // the build skipped every removed track's postings
     return AID_OK;
 }
 
@@ -1282,9 +1285,10 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // global histogram: ~2 buckets per expected vote keeps chance buckets >= min_match rare
     int bits = 16;
     while (bits < 24 && (double)(1ull << bits) < 2.0 * votes) ++bits;
-    // LDS fast path only while its 2^16 counters stay sparse (same load bound). Heavier
-    // queries are exact on it too (tests/test_gpu_match_load.py) but slower than the global path
-    // (one 16-wave workgroup per CU: 76.7 s against 1.42 s for config 4's 33k windows)
+    // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is
+    // exact for heavier queries too (overflows fall back; tests/test_gpu_match_load.py) but one
+    // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~180k
+    // votes each) take 48.6 s on it against 1.43 s on the global path
     const bool fast = e->k5_path == 1 || (e->k5_path == 0 && 2.0 * votes <= 65536.0);
     // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
     // through to the global-histogram path below
@@ -1292,7 +1296,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         {
             ProfScope ps(e, AID_K_MATCH, s);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, s);
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, s);
         }
         HIP_TRY(hipGetLastError());
         std::vector<int32_t> got_n(nq);

@@ -132,7 +132,74 @@ struct QueryParams {
     int32_t hist_bits;
     int32_t *rows;             // [nq][max_rows][5]
     int32_t *nrows;            // [nq]; -1 = LDS table overflow (query not answered)
+    int32_t tomb_live;         // 0: the CSR holds no posting of a removed track (skip tomb[] loads)
 };
+
+// Every vote (track, d = t_ref - t_q, t_q) of query records [a, a + n), for the calling wave's
+// share of the records, with all 64 lanes on postings: the wave takes 64 records (one per
+// lane: key, bucket start and length), scans the lengths, then walks the concatenated postings
+// 64 at a time -- a lane finds its record among the few whose ranges meet the 64-posting window
+// (ballot + readlane, scalar loop) -- with U windows' posting loads in flight before use. (One
+// record per wave with lanes over its ~10-200 postings left most lanes idle and serialised
+// recs -> offsets -> post -> tomb round trips per record.)
+template <int U, typename F>
+__device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
+                                              F &&f) {
+    for (int64_t base = (int64_t)wave * 64; base < n; base += (int64_t)nw * 64) {
+        const int64_t i = base + lane;
+        uint32_t p0 = 0, len = 0;
+        int32_t tq = 0;
+        if (i < n) {
+            const uint64_t r = qp.recs[a + i];
+            const uint32_t k = key26((uint32_t)r);
+            tq = (int32_t)(r >> 32);
+            p0 = qp.offsets[k];
+            len = qp.offsets[k + 1] - p0;
+        }
+        uint32_t incl = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        const uint32_t excl = incl - len;
+        const uint32_t total = __shfl(incl, 63);
+        for (uint32_t w0 = 0; w0 < total; w0 += 64u * U) {
+            uint32_t pos[U];
+            int32_t tqs[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t lo = w0 + 64u * u, j = lo + lane;
+                pos[u] = 0xFFFFFFFFu;
+                tqs[u] = 0;
+                if (lo >= total) continue;  // uniform
+                // records whose range [excl, incl) meets [lo, lo + 64): usually 1-2
+                uint64_t m = __ballot(len > 0 && excl < lo + 64u && incl > lo);
+                while (m) {
+                    const int rl = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t e0 = __shfl(excl, rl), e1 = __shfl(incl, rl);
+                    const uint32_t pp = __shfl(p0, rl);
+                    const int32_t tr = __shfl(tq, rl);
+                    if (j >= e0 && j < e1) {
+                        pos[u] = pp + (j - e0);
+                        tqs[u] = tr;
+                    }
+                }
+            }
+            uint64_t e[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) e[u] = pos[u] != 0xFFFFFFFFu ? qp.post[pos[u]] : 0ull;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (pos[u] == 0xFFFFFFFFu) continue;
+                const uint32_t trk = (uint32_t)e[u];
+                if (qp.tomb_live && qp.tomb[trk]) continue;
+                f(trk, (int32_t)(e[u] >> 32) - tqs[u], tqs[u]);
+            }
+        }
+    }
+}
 
 // one wave per query record; its lanes stride over the record's posting list (coalesced)
 __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
@@ -326,26 +393,17 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
     __syncthreads();
     const bool check_wrap = L.votes >= 0xFFFFu;
     // phase 1
-    for (int64_t i = wave; i < n; i += nw) {
-        const uint64_t r = qp.recs[a + i];
-        const uint32_t k = key26((uint32_t)r);
-        const int32_t tq = (int32_t)(r >> 32);
-        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
-        for (uint32_t p = p0 + lane; p < p1; p += 64) {
-            const uint64_t e = qp.post[p];
-            const uint32_t tr = (uint32_t)e;
-            if (qp.tomb[tr]) continue;
-            const uint32_t h = mix_td(tr, (int32_t)(e >> 32) - tq) & hmask;
-            if (check_wrap) {
-                const uint32_t old = atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
-                // a 16-bit counter at 0xFFFF would carry into its neighbour: hand the query to
-                // the global path (exactness over speed)
-                if (((old >> (16 * (h & 1))) & 0xFFFFu) == 0xFFFFu) L.overflow = 1;
-            } else {
-                atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
-            }
+    for_each_vote<4>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
+        const uint32_t h = mix_td(tr, d) & hmask;
+        if (check_wrap) {
+            const uint32_t old = atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
+            // a 16-bit counter at 0xFFFF would carry into its neighbour: hand the query to
+            // the global path (exactness over speed)
+            if (((old >> (16 * (h & 1))) & 0xFFFFu) == 0xFFFFu) L.overflow = 1;
+        } else {
+            atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
         }
-    }
+    });
     __syncthreads();
     if (L.overflow) {  // uniform: the global path answers this query
         if (tid == 0) qp.nrows[q] = -1;
@@ -375,35 +433,25 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
     }
     __syncthreads();
     // phase 3
-    for (int64_t i = wave; i < n; i += nw) {
-        const uint64_t r = qp.recs[a + i];
-        const uint32_t k = key26((uint32_t)r);
-        const int32_t tq = (int32_t)(r >> 32);
-        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
-        for (uint32_t p = p0 + lane; p < p1; p += 64) {
-            const uint64_t e = qp.post[p];
-            const uint32_t tr = (uint32_t)e;
-            if (qp.tomb[tr]) continue;
-            const int32_t d = (int32_t)(e >> 32) - tq;
-            const uint32_t hf = mix_td(tr, d);
-            const uint32_t h = hf & hmask;
-            if (!((L.hot[h >> 5] >> (h & 31)) & 1u)) continue;
-            const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
-            uint32_t s = (hf >> 20) & (kFastVoteCap - 1);
-            int probes = 0;
-            for (;;) {
-                const unsigned long long old = atomicCAS(&L.u.t.vkey[s], ~0ull, key);
-                if (old == ~0ull || old == key) {
-                    atomicAdd(&L.u.t.vcnt[s], 1u);
-                    atomicMin(&L.u.t.vmin[s], (uint32_t)tq);
-                    atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
-                    break;
-                }
-                if (++probes >= kFastVoteCap) { L.overflow = 1; break; }
-                s = (s + 1) & (kFastVoteCap - 1);
+    for_each_vote<4>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
+        const uint32_t hf = mix_td(tr, d);
+        const uint32_t h = hf & hmask;
+        if (!((L.hot[h >> 5] >> (h & 31)) & 1u)) return;
+        const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
+        uint32_t s = (hf >> 20) & (kFastVoteCap - 1);
+        int probes = 0;
+        for (;;) {
+            const unsigned long long old = atomicCAS(&L.u.t.vkey[s], ~0ull, key);
+            if (old == ~0ull || old == key) {
+                atomicAdd(&L.u.t.vcnt[s], 1u);
+                atomicMin(&L.u.t.vmin[s], (uint32_t)tq);
+                atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
+                break;
             }
+            if (++probes >= kFastVoteCap) { L.overflow = 1; break; }
+            s = (s + 1) & (kFastVoteCap - 1);
         }
-    }
+    });
     __syncthreads();
     // phase 4: best d per track
     for (int s = tid; s < kFastVoteCap; s += kFastThreads) {
@@ -465,9 +513,10 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
 
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
-                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, hipStream_t s) {
+                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s) {
     if (nq <= 0) return;
-    QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows};
+    QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
+                   tomb_live};
     hipLaunchKernelGGL(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
 }
 
@@ -503,7 +552,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
                   uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
-                   nrows};
+                   nrows, 1};
     hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
