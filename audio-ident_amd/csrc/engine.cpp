@@ -51,7 +51,7 @@ void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, co
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
-                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s);
+                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
@@ -1343,7 +1343,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             {
                 ProfScope ps(e, AID_K_MATCH, s);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_hist.p, bits, out_rows + (size_t)q0 * mr * 5, out_n + q0, s);
+                             e->cfg.min_match, mr, e->q_hist.p, bits, out_rows + (size_t)q0 * mr * 5, out_n + q0,
+                             e->tomb_since_build > 0, s);
             }
             HIP_TRY(hipGetLastError());
         }

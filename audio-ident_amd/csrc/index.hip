@@ -205,22 +205,11 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
 __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
     const int q = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
+    const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t hmask = (1u << qp.hist_bits) - 1;
     uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
-    for (int64_t i = a + wave; i < z; i += nw) {
-        const uint64_t r = qp.recs[i];
-        const uint32_t k = key26((uint32_t)r);
-        const int32_t tq = (int32_t)(r >> 32);
-        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
-        for (uint32_t p = p0 + lane; p < p1; p += 64) {
-            const uint64_t e = qp.post[p];
-            const uint32_t tr = (uint32_t)e;
-            if (qp.tomb[tr]) continue;
-            const int32_t d = (int32_t)(e >> 32) - tq;
-            atomicAdd(&H[mix_td(tr, d) & hmask], 1u);
-        }
-    }
+    for_each_vote<4>(qp, a, n, wave, nw, lane,
+                     [&](uint32_t tr, int32_t d, int32_t) { atomicAdd(&H[mix_td(tr, d) & hmask], 1u); });
 }
 
 __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
@@ -250,35 +239,25 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
     const uint32_t mm = (uint32_t)qp.min_match;
     const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-    // 1. exact table of candidate votes (one wave per record, lanes over its postings)
-    for (int64_t i = a + wave; i < z; i += nw) {
-        const uint64_t r = qp.recs[i];
-        const uint32_t k = key26((uint32_t)r);
-        const int32_t tq = (int32_t)(r >> 32);
-        const uint32_t p0 = qp.offsets[k], p1 = qp.offsets[k + 1];
-        for (uint32_t p = p0 + lane; p < p1; p += 64) {
-            const uint64_t e = qp.post[p];
-            const uint32_t tr = (uint32_t)e;
-            if (qp.tomb[tr]) continue;
-            const int32_t d = (int32_t)(e >> 32) - tq;
-            const uint32_t h = mix_td(tr, d);
-            if (H[h & hmask] < mm) continue;
-            const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
-            uint32_t s = (h >> 20) & (kVoteCap - 1);
-            int probes = 0;
-            for (;;) {
-                const unsigned long long old = atomicCAS(&vkey[s], ~0ull, key);
-                if (old == ~0ull || old == key) {
-                    atomicAdd(&vcnt[s], 1u);
-                    atomicMin(&vmin[s], (uint32_t)tq);
-                    atomicMax(&vmax[s], (uint32_t)tq);
-                    break;
-                }
-                if (++probes >= kVoteCap) { overflow = 1; break; }
-                s = (s + 1) & (kVoteCap - 1);
+    // 1. exact table of candidate votes
+    for_each_vote<4>(qp, a, z - a, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
+        const uint32_t h = mix_td(tr, d);
+        if (H[h & hmask] < mm) return;
+        const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
+        uint32_t s = (h >> 20) & (kVoteCap - 1);
+        int probes = 0;
+        for (;;) {
+            const unsigned long long old = atomicCAS(&vkey[s], ~0ull, key);
+            if (old == ~0ull || old == key) {
+                atomicAdd(&vcnt[s], 1u);
+                atomicMin(&vmin[s], (uint32_t)tq);
+                atomicMax(&vmax[s], (uint32_t)tq);
+                break;
             }
+            if (++probes >= kVoteCap) { overflow = 1; break; }
+            s = (s + 1) & (kVoteCap - 1);
         }
-    }
+    });
     __syncthreads();
     // 2. best d per track: max count, then smallest d
     for (int s = tid; s < kVoteCap; s += blockDim.x) {
@@ -549,10 +528,10 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
-                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, hipStream_t s) {
+                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
-                   nrows, 1};
+                   nrows, tomb_live};
     hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
