@@ -51,7 +51,8 @@ void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, co
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
-                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s);
+                  uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
+                  hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
@@ -149,6 +150,7 @@ struct aid_engine {
     DevBuf<int64_t> q_start, q_count;
     DevBuf<uint32_t> q_hist;
     DevBuf<int32_t> q_rows, q_nrows;
+    DevBuf<uint32_t> q_hot;  // K5h hot-bucket bitmaps, [batch][2^bits / 32]
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
     DevBuf<float> x_in, x_win;
@@ -346,6 +348,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->q_start.release();
     e->q_count.release();
     e->q_hist.release();
+    e->q_hot.release();
     e->q_rows.release();
     e->q_nrows.release();
     e->x_src.release();
@@ -1317,6 +1320,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         const size_t H = (size_t)1 << bits;
         const int batch = (int)std::max<size_t>(1, std::min<size_t>(2048, ((size_t)4 << 30) / (H * 4)));
         HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
+        HIP_TRY(e->q_hot.reserve((size_t)std::min<int>((int)todo.size(), batch) * (H / 32)));
         if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5b re-zeroes its rows afterwards
             HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
             e->hist_zero_cap = e->q_hist.n;
@@ -1343,8 +1347,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             {
                 ProfScope ps(e, AID_K_MATCH, s);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_hist.p, bits, out_rows + (size_t)q0 * mr * 5, out_n + q0,
-                             e->tomb_since_build > 0, s);
+                             e->cfg.min_match, mr, e->q_hist.p, bits, e->q_hot.p, out_rows + (size_t)q0 * mr * 5,
+                             out_n + q0, e->tomb_since_build > 0, s);
             }
             HIP_TRY(hipGetLastError());
         }

@@ -133,6 +133,7 @@ struct QueryParams {
     int32_t *rows;             // [nq][max_rows][5]
     int32_t *nrows;            // [nq]; -1 = LDS table overflow (query not answered)
     int32_t tomb_live;         // 0: the CSR holds no posting of a removed track (skip tomb[] loads)
+    uint32_t *hot;             // [nq][2^hist_bits / 32] bit per histogram bucket >= min_match (K5h)
 };
 
 // Every vote (track, d = t_ref - t_q, t_q) of query records [a, a + n), for the calling wave's
@@ -212,6 +213,25 @@ __global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
                      [&](uint32_t tr, int32_t d, int32_t) { atomicAdd(&H[mix_td(tr, d) & hmask], 1u); });
 }
 
+// K5h: one coalesced pass over each query's histogram row: bucket >= min_match -> a bit of the
+// row's hot bitmap (64 counters per wave ballot), and the row is zeroed for the next batch.
+// K5b then tests 4-byte words of a 64 KB bitmap (L2-resident) instead of gathering its votes'
+// counters from the 2 MB row (a 64-128 B line per 4-byte read: ~46 GB of fetch per 2048 queries).
+__global__ __launch_bounds__(256) void k_hot_scan(QueryParams qp) {
+    const int64_t per_q = 1ll << qp.hist_bits;
+    const uint32_t mm = (uint32_t)qp.min_match;
+    for (int q = blockIdx.y; q < qp.nq; q += gridDim.y) {
+        uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
+        uint64_t *B = reinterpret_cast<uint64_t *>(qp.hot + ((int64_t)q << (qp.hist_bits - 5)));
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per_q; i += (int64_t)gridDim.x * 256) {
+            const uint32_t c = H[i];
+            const uint64_t m = __ballot(c >= mm);
+            if ((threadIdx.x & 63) == 0) B[i >> 6] = m;  // i of lane 0 is a multiple of 64
+            H[i] = 0u;
+        }
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     __shared__ unsigned long long vkey[kVoteCap];  // (track << 32) | (uint32)d ; ~0 = empty
     __shared__ uint32_t vcnt[kVoteCap], vmin[kVoteCap], vmax[kVoteCap];
@@ -236,13 +256,14 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     __syncthreads();
     const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
     const uint32_t hmask = (1u << qp.hist_bits) - 1;
-    uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
+    const uint32_t *hot = qp.hot + ((int64_t)q << (qp.hist_bits - 5));
     const uint32_t mm = (uint32_t)qp.min_match;
     const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     // 1. exact table of candidate votes
     for_each_vote<4>(qp, a, z - a, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
         const uint32_t h = mix_td(tr, d);
-        if (H[h & hmask] < mm) return;
+        const uint32_t hb = h & hmask;
+        if (!((hot[hb >> 5] >> (hb & 31)) & 1u)) return;
         const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
         uint32_t s = (h >> 20) & (kVoteCap - 1);
         int probes = 0;
@@ -314,8 +335,6 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
         }
     }
     if (tid == 0) qp.nrows[q] = (overflow || out_n > kTrackCap) ? -1 : min(n, qp.max_rows);
-    // 5. re-zero this query's histogram row
-    for (int64_t i = tid; i <= (int64_t)hmask; i += blockDim.x) H[i] = 0u;
 }
 
 // ---- K5 (fast path): the whole vote filter in LDS, one 1024-thread workgroup per query ----
@@ -495,7 +514,7 @@ void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t
                       int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
-                   tomb_live};
+                   tomb_live, nullptr};
     hipLaunchKernelGGL(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
 }
 
@@ -528,11 +547,13 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
-                  uint32_t *hist, int hist_bits, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s) {
+                  uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
+                  hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
-                   nrows, tomb_live};
+                   nrows, tomb_live, hot};
     hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
+    hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
 
