@@ -187,6 +187,7 @@ struct aid_engine {
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
     int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
+    size_t k5_batch = 2048;        // global-path queries per launch (AIDFP_K5_BATCH)
     hipStream_t last_stream = nullptr;
     bool have_result = false;
 
@@ -292,6 +293,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
+    if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
     hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
@@ -1318,7 +1320,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     for (int attempt = 1; !todo.empty(); ++attempt, bits += 2) {
         if (bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
         const size_t H = (size_t)1 << bits;
-        const int batch = (int)std::max<size_t>(1, std::min<size_t>(2048, ((size_t)4 << 30) / (H * 4)));
+        const int batch = (int)std::max<size_t>(1, std::min<size_t>(e->k5_batch, ((size_t)4 << 30) / (H * 4)));
         HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
         HIP_TRY(e->q_hot.reserve((size_t)std::min<int>((int)todo.size(), batch) * (H / 32)));
         if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5b re-zeroes its rows afterwards

@@ -203,7 +203,10 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
 }
 
 // one wave per query record; its lanes stride over the record's posting list (coalesced)
-__global__ __launch_bounds__(256) void k_vote_hist(QueryParams qp) {
+#ifndef AID_K5_HIST_THREADS
+#define AID_K5_HIST_THREADS 1024  // 256: 9.4k clips/s on config 4, 1024: 10.3k
+#endif
+__global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams qp) {
     const int q = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
@@ -552,7 +555,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
                    nrows, tomb_live, hot};
-    hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(256), 0, s, qp);
+    hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
     hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
