@@ -206,14 +206,32 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
 #ifndef AID_K5_HIST_THREADS
 #define AID_K5_HIST_THREADS 1024  // 256: 9.4k clips/s on config 4, 1024: 10.3k
 #endif
+#ifndef AID_K5_SEEN
+#define AID_K5_SEEN 1  // LDS "seen" pre-filter in front of the global histogram (see k_vote_hist)
+#endif
+// K5a. With AID_K5_SEEN a vote first sets its key's bit in a 2^20-bit LDS bitmap (128 KB) and
+// reaches the global histogram only if the bit was already set: of a key's c votes at most the
+// first is held back, so a bucket holding a key with c >= min_match votes still counts
+// >= min_match - 1 (K5h tests that). Most chance votes are first occurrences (~180k votes over
+// 2^20 bits: ~8 % collide), so the random global atomics -- the kernel's cost -- drop ~10x.
 __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams qp) {
     const int q = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t hmask = (1u << qp.hist_bits) - 1;
     uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
+#if AID_K5_SEEN
+    __shared__ uint32_t seen[1 << 15];
+    for (int i = threadIdx.x; i < (1 << 15); i += blockDim.x) seen[i] = 0u;
+    __syncthreads();
+    for_each_vote<4>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
+        const uint32_t x = mix_td(tr, d), b = x >> 12, bit = 1u << (b & 31);
+        if (atomicOr(&seen[b >> 5], bit) & bit) atomicAdd(&H[x & hmask], 1u);
+    });
+#else
     for_each_vote<4>(qp, a, n, wave, nw, lane,
                      [&](uint32_t tr, int32_t d, int32_t) { atomicAdd(&H[mix_td(tr, d) & hmask], 1u); });
+#endif
 }
 
 // K5h: one coalesced pass over each query's histogram row: bucket >= min_match -> a bit of the
@@ -222,7 +240,7 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
 // counters from the 2 MB row (a 64-128 B line per 4-byte read: ~46 GB of fetch per 2048 queries).
 __global__ __launch_bounds__(256) void k_hot_scan(QueryParams qp) {
     const int64_t per_q = 1ll << qp.hist_bits;
-    const uint32_t mm = (uint32_t)qp.min_match;
+    const uint32_t mm = (uint32_t)qp.min_match - (AID_K5_SEEN ? 1u : 0u);  // see k_vote_hist
     for (int q = blockIdx.y; q < qp.nq; q += gridDim.y) {
         uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
         uint64_t *B = reinterpret_cast<uint64_t *>(qp.hot + ((int64_t)q << (qp.hist_bits - 5)));
