@@ -1287,7 +1287,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         for (int q = 0; q < nq; ++q) max_recs = std::max(max_recs, h_count[q]);
     const double per_bucket = e->n_buckets_used > 0 ? (double)e->n_indexed / (double)e->n_buckets_used : 1.0;
     const double votes = std::max(1.0, (double)max_recs * per_bucket);
-    // global histogram: ~2 buckets per expected vote keeps chance buckets >= min_match rare
+    // global histogram: ~2 buckets per expected vote. (Sizing it for the ~10 % of votes that
+    // pass K5a's seen filter measured slower: 20.5k against 27.2k clips/s on config 4.)
     int bits = 16;
     while (bits < 24 && (double)(1ull << bits) < 2.0 * votes) ++bits;
     // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is

@@ -206,6 +206,9 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
 #ifndef AID_K5_HIST_THREADS
 #define AID_K5_HIST_THREADS 1024  // 256: 9.4k clips/s on config 4, 1024: 10.3k
 #endif
+#ifndef AID_K5_U
+#define AID_K5_U 16  // 64-posting windows with loads in flight per wave in K5a/K5b (4: 26.9k clips/s, 8: 27.9k, 16: 28.3k)
+#endif
 #ifndef AID_K5_SEEN
 #define AID_K5_SEEN 1  // LDS "seen" pre-filter in front of the global histogram (see k_vote_hist)
 #endif
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
     __shared__ uint32_t seen[1 << 15];
     for (int i = threadIdx.x; i < (1 << 15); i += blockDim.x) seen[i] = 0u;
     __syncthreads();
-    for_each_vote<4>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
+    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
         const uint32_t x = mix_td(tr, d), b = x >> 12, bit = 1u << (b & 31);
         if (atomicOr(&seen[b >> 5], bit) & bit) atomicAdd(&H[x & hmask], 1u);
     });
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     const uint32_t mm = (uint32_t)qp.min_match;
     const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     // 1. exact table of candidate votes
-    for_each_vote<4>(qp, a, z - a, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
+    for_each_vote<AID_K5_U>(qp, a, z - a, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
         const uint32_t h = mix_td(tr, d);
         const uint32_t hb = h & hmask;
         if (!((hot[hb >> 5] >> (hb & 31)) & 1u)) return;

@@ -140,7 +140,10 @@ def lane(args, eng, st, truth, starts, n_pos, n_neg, t_index) -> int:
     t_gpu = 0.0
     top1 = fp_hits = 0
     off_err = []
-    eng.exact_lane(pcm_ptr=pcm.data_ptr(), offsets=np.arange(2, dtype=np.int64) * clip_n, max_out=10)  # warm
+    # warm-up: one full batch, untimed (first-use device allocations: vote histogram, bitmaps, rows)
+    qs = np.arange(0, min(nq, args.batch))
+    eng.synth(pcm.data_ptr(), truth[qs], starts[qs], clip_n, noise_a=noise_a, salt=77)
+    eng.exact_lane(pcm_ptr=pcm.data_ptr(), offsets=np.arange(len(qs) + 1, dtype=np.int64) * clip_n, max_out=10)
     for q0 in range(0, nq, args.batch):
         qs = np.arange(q0, min(nq, q0 + args.batch))
         eng.synth(pcm.data_ptr(), truth[qs], starts[qs], clip_n, noise_a=noise_a, salt=77)
