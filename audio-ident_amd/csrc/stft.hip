@@ -64,10 +64,12 @@ namespace aid {
 // pairs; the readers (k = lane + 64i, and the mirror 1024-k) stay a permutation of one or two
 // 16-entry blocks, so every access is conflict-free (the mirror read: one 2-way pair per wave).
 #if AID_K1_DPPC
-// E3 slot of Z[k] (DPP stage C): bit 4 ^= bit 9. Writers (k = kq + 16 j1 + 256 j2, one j1 per
-// instruction) then hit 32 distinct 8-byte bank pairs twice each; the real split reads Z[k] for
-// k < 512 unswizzled and the mirrors (>= 512) with bit 4 flipped, both conflict-free.
-__device__ __forceinline__ int e3(int k) { return k ^ (((k >> 9) & 1) << 4); }
+// E3 slot of Z[k] (DPP stage C): bit 3 ^= bit 8, bit 4 ^= bit 9. A b64 access is served per half
+// wave (32 lanes on the 32 8-byte bank pairs); the writers of one half (k = kq + 16 j1 + 256 j2,
+// kq < 8 or >= 8, one j1 per instruction) then cover 32 distinct pairs, and so do the real
+// split's readers Z[lane + 64 i] (lane ^ const) and their mirrors (one 2-way pair from lane 0).
+// (With bit 4 ^= bit 9 alone a half's writers hit 16 pairs: 34 % of LDS cycles were conflicts.)
+__device__ __forceinline__ int e3(int k) { return k ^ (((k >> 8) & 1) << 3) ^ (((k >> 9) & 1) << 4); }
 // partner value across the lane quad (DPP quad_perm; every lane of the quad is valid)
 template <int CTRL>
 __device__ __forceinline__ float quad_dpp(float x) {
@@ -104,9 +106,15 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #if AID_K1_DPPC
     // writer slots: e3(kq + 16 j1 + 256 j2) = kq + 256 j2 + 16 (j1 ^ (j2 >> 1)) = base[j1 & 1] + 16 j1
     const int j2q = ((mq & 1) << 1) | (mq >> 1);  // lane mq holds output j2 = bitrev2(mq)
-    const int e3w0 = kq + 256 * j2q + 16 * (j2q >> 1), e3w1 = kq + 256 * j2q - 16 * (j2q >> 1);
-    const int e3a = lane;                            // Z[lane + 64 i], i < 8: bit 9 clear
-    const int e3b = (lane == 0) ? 80 : ((64 - lane) ^ 16);  // Z[64 (15 - i) + 64 - lane] ^ 16
+    // writer slots: e3(kq + 16 j1 + 256 j2) = (kq ^ 8 (j2 & 1)) + 256 j2 + 16 (j1 ^ (j2 >> 1))
+    const int e3k = (kq ^ ((j2q & 1) << 3)) + 256 * j2q;
+    const int e3w0 = e3k + 16 * (j2q >> 1), e3w1 = e3k - 16 * (j2q >> 1);  // j1 even / odd (+ 16 j1)
+    // readers: Z[lane + 64 i] (i < 8: bit 9 clear, bit 8 = i >> 2) -> e3a[i >> 2] + 64 i;
+    // Z[1024 - lane - 64 i] = Z[64 (15 - i) + m], m = 64 - lane (bit 9 set, bit 8 = i < 4)
+    //   -> e3b[i < 4] + 64 (15 - i); lane 0 (m = 64, Z[64 (16 - i)]) matches that except at i = 4
+    const int e3a0 = lane, e3a1 = lane ^ 8;
+    const int e3b1 = (64 - lane) ^ 24, e3b0 = (lane == 0) ? 80 : ((64 - lane) ^ 16);
+    const int e3b4 = (lane == 0) ? 88 : e3b0;  // i = 4: Z[768] for lane 0
     const float s1 = mq < 2 ? 1.0f : -1.0f;                     // butterfly over lanes (mq, mq ^ 2)
     const float s2 = (mq == 1 || mq == 2) ? -1.0f : 1.0f;       // butterfly over lanes (mq, mq ^ 1)
     const float s0 = lane == 0 ? 1.0f : -1.0f;  // sign of Z[0]'s mirror slot for i = 0 (Z[0] itself)
@@ -326,9 +334,15 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const int k = lane + 64 * i;  // 0..511
+#if AID_K1_DPPC
+                    const float2 a = buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
+                    // k = 0 mirrors onto itself (Z[0]: slot 0)
+                    const int bi = (i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
+#else
                     const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[e3a + 64 * i];
                     // k = 0 mirrors onto itself (Z[0]): lane 0's e3b + 960 would be slot 1024
                     const int bi = (i == 0 && lane == 0) ? 0 : e3b + 64 * (15 - i);
+#endif
 #if AID_K1_DPPC
                     // stored Z[k] is -Z[k] for k >= 256 (lanes 1..3 of stage C): for i < 4, a is exact
                     // and b is stored negated (except Z[0] for lane 0, i = 0), so flip b; for i >= 4 both
