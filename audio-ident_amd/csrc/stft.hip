@@ -31,7 +31,10 @@
 //   1 = E3 writes lane-contiguous, 2 = real-split mirror reads lane-contiguous,
 //   4 = E1 read lane-contiguous, 5 = E2 read lane-contiguous,
 //   6 = no E1 exchange, 7 = no E2 exchange, 8 = no E3 exchange (real split on registers),
-//   9 = no stage A/B DFT16 arithmetic, 10 = one float stored per lane and frame (not 16 rows)
+//   9 = no stage A/B DFT16 arithmetic, 10 = one float stored per lane and frame (not 16 rows),
+//   11 = the 16 rows stored as 4 dwordx4 per lane (same bytes, a quarter of the store instructions)
+// Round-1 ablation of the DPP build (one box, K1 0.343 ms): no E1 0.306, no E3 0.306, no DFT16
+// arithmetic 0.312, no power stores 0.310, dwordx4 stores 0.346 -- no single phase dominates.
 #ifndef AID_K1_DIAG
 #define AID_K1_DIAG 0
 #endif
@@ -285,7 +288,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     v[j0 + 2] = make_float2(u2, w2);
                     v[j0 + 3] = make_float2(u3, w3);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) buf[e3w + 16 * (j0 + j)] = v[j0 + j];
+                    for (int j = 0; j < 4; ++j)
+                        if (AID_K1_DIAG != 8) buf[e3w + 16 * (j0 + j)] = v[j0 + j];
                 }
 #else
 #pragma unroll
@@ -328,6 +332,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 wave_lds_sync();
                 float *drow = dst + (int64_t)f * kBins;
                 float acc10 = 0.f;
+                float pv11[16];  // AID_K1_DIAG 11: the lane's 16 powers, stored as 4 dwordx4 (timing only)
                 // real split, bins in mirror pairs (k, 1024-k): one read of Z[k], Z[1024-k] serves
                 // both. For bin 1024-k the FPSPEC sums are the same exact values with signs
                 // flipped (a+c, c+a commute; b-d = -(d-b)), so both bins stay bit-exact.
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 for (int i = 0; i < 8; ++i) {
                     const int k = lane + 64 * i;  // 0..511
 #if AID_K1_DPPC
-                    const float2 a = buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
+                    const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
                     // k = 0 mirrors onto itself (Z[0]: slot 0)
                     const int bi = (i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
 #else
@@ -347,7 +352,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     // stored Z[k] is -Z[k] for k >= 256 (lanes 1..3 of stage C): for i < 4, a is exact
                     // and b is stored negated (except Z[0] for lane 0, i = 0), so flip b; for i >= 4 both
                     // are negated, every sum below flips sign and the squares in P do not see it
-                    const float2 bs = buf[bi];
+                    const float2 bs = AID_K1_DIAG == 8 ? v[15 - i] : buf[bi];
                     const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
 #else
                     const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[AID_K1_DIAG == 2 ? e3(k ^ 512) : bi];
@@ -361,6 +366,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                         if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
                         else if (AID_K1_DIAG == 10) acc10 += P;
+                        else if (AID_K1_DIAG == 11) pv11[2 * i] = P;
                         else drow[k] = P;
                     }
                     if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
@@ -369,10 +375,19 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                         if constexpr (LOGMAG) drow[1024 - k] = 10.0f * log10f(P + 1e-10f);
                         else if (AID_K1_DIAG == 10) acc10 += P;
+                        else if (AID_K1_DIAG == 11) pv11[2 * i + 1] = P;
                         else drow[1024 - k] = P;
+                    } else if (AID_K1_DIAG == 11) {
+                        pv11[2 * i + 1] = 0.f;
                     }
                 }
                 if (AID_K1_DIAG == 10) drow[lane] = acc10;
+                if (AID_K1_DIAG == 11) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        reinterpret_cast<float4 *>(drow)[64 * q + lane] =
+                            make_float4(pv11[4 * q], pv11[4 * q + 1], pv11[4 * q + 2], pv11[4 * q + 3]);
+                }
                 if (lane == 0) {  // bin 512 pairs with itself
                     const float2 a = buf[e3(512)];
                     const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
