@@ -31,6 +31,9 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_REVERSE
 #define AID_K2_REVERSE 1  // 1: last-written strips first (0.2975 -> 0.2930 ms, A/B on one box)
 #endif
+#ifndef AID_K2_BLOCKMAX
+#define AID_K2_BLOCKMAX 1  // horizontal maxima from 4-bin block maxima (see below); 0 = 36 values per thread
+#endif
 #ifndef AID_K2_PF
 #define AID_K2_PF 4  // prefetch distance in rows (4 or 8): rows it+PF .. are in flight in registers
 #endif
@@ -53,6 +56,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
                                                   uint64_t *__restrict__ mask) {
     __shared__ __attribute__((aligned(16))) int rows[2][kRowsPerStep][kBins + 32];
+#if AID_K2_BLOCKMAX
+    __shared__ __attribute__((aligned(16))) int bms[2][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
+#endif
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -90,6 +96,12 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             for (int r = 0; r < kRowsPerStep; ++r) {
                 rows[b][r][tid] = 0;
                 rows[b][r][kBins + 16 + tid] = 0;
+#if AID_K2_BLOCKMAX
+                if (tid < 4) {
+                    bms[b][r][tid] = 0;
+                    bms[b][r][260 + tid] = 0;
+                }
+#endif
             }
     }
 
@@ -132,7 +144,11 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 for (int j = 0; j < kRowsPerStep; ++j) {
                     const int slot = (s + j) % AID_K2_PF;  // compile-time: the loop is unrolled by 8
                     const float4 v = pf[slot];
-                    reinterpret_cast<int4 *>(&rows[buf][j][16])[tid] = make_int4(pkey(v.x), pkey(v.y), pkey(v.z), pkey(v.w));
+                    const int4 kv = make_int4(pkey(v.x), pkey(v.y), pkey(v.z), pkey(v.w));
+                    reinterpret_cast<int4 *>(&rows[buf][j][16])[tid] = kv;
+#if AID_K2_BLOCKMAX
+                    bms[buf][j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
+#endif
                     const int rn = rbeg + it + j + AID_K2_PF;
                     pf[slot] = (it + j + AID_K2_PF < iters && rn >= 0 && rn < F)
                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
@@ -141,7 +157,35 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 __syncthreads();
             }
             const int r = rbeg + it;
+#if !AID_K2_BLOCKMAX
             const int *rb = rows[buf][s % kRowsPerStep];
+#endif
+#if AID_K2_BLOCKMAX
+            // thread j owns block j = bins 4j..4j+3. Its +-15 windows span blocks j-4..j+4: the
+            // far blocks j-4 / j+4 contribute a suffix / prefix of their bins, blocks j+-1..3 whole
+            // (their maxima, staged with the row), the own block a prefix / suffix -- 18 max ops
+            // per thread and row instead of 46, and 2 x 16 B + 6 x 4 B of LDS reads instead of 9 x 16 B
+            const int4 *rb4 = reinterpret_cast<const int4 *>(rows[buf][s % kRowsPerStep]);
+            const int *bm = bms[buf][s % kRowsPerStep];
+            const int4 lf = rb4[tid], me = rb4[tid + 4], rt = rb4[tid + 8];  // blocks j-4, j, j+4
+            const int M3L = max(max(bm[tid + 1], bm[tid + 2]), bm[tid + 3]);  // blocks j-3..j-1
+            const int M3R = max(max(bm[tid + 5], bm[tid + 6]), bm[tid + 7]);  // blocks j+1..j+3
+            const int lsuf2 = max(lf.z, lf.w), lsuf1 = max(lf.y, lsuf2);      // block j-4: bins 1..3, 2..3
+            const int rpre1 = max(rt.x, rt.y), rpre2 = max(rpre1, rt.z);      // block j+4: bins 0..1, 0..2
+            const int mpre1 = max(me.x, me.y), mpre2 = max(mpre1, me.z);      // own prefixes
+            const int msuf2 = max(me.z, me.w), msuf1 = max(me.y, msuf2);      // own suffixes
+            int L[4], R[4];
+            L[0] = max(lsuf1, M3L);
+            L[1] = max(max(lsuf2, M3L), me.x);
+            L[2] = max(max(lf.w, M3L), mpre1);
+            L[3] = max(M3L, mpre2);
+            R[0] = max(msuf1, M3R);
+            R[1] = max(max(msuf2, M3R), rt.x);
+            R[2] = max(max(me.w, M3R), rpre1);
+            R[3] = max(M3R, rpre2);
+            int q[36];
+            q[16] = me.x; q[17] = me.y; q[18] = me.z; q[19] = me.w;
+#else
             int q[36];  // bins 4j-16 .. 4j+19 (zero outside the frame)
 #pragma unroll
             for (int v = 0; v < 9; ++v) {
@@ -166,6 +210,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             R[1] = max(max(q[18], q[19]), max(midR, q[32]));
             R[2] = max(max(q[19], midR), max(q[32], q[33]));
             R[3] = max(max(midR, q[32]), max(q[33], q[34]));
+#endif
 
             // candidates only inside the strip's output rows (uniform): other rows get +inf
             const int thr_row = (r >= t0 && r < t1) ? kthr : kInf;
