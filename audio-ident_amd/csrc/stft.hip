@@ -45,6 +45,9 @@
 #endif
 // AID_K1_BALANCED=1 (default): waves take equal frame ranges of the whole batch (ring restarts
 // only at clip edges) instead of 16-frame strips; 0 = strips (A/B)
+#ifndef AID_K1_PRIO
+#define AID_K1_PRIO 0  // s_setprio level around the E1 exchange (experiment)
+#endif
 #ifndef AID_K1_BALANCED
 #define AID_K1_BALANCED 1
 #endif
@@ -217,6 +220,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
                     v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
                 }
+#if AID_K1_PRIO
+                __builtin_amdgcn_s_setprio(AID_K1_PRIO);  // exchange phase: keep the LDS queue fed
+#endif
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
                 if (AID_K1_DIAG != 6) {
 #pragma unroll
@@ -231,6 +237,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     wave_lds_sync();
                 }
                 // stage B
+#if AID_K1_PRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
                 if (AID_K1_DIAG != 9) dft16(v, t16);
 #pragma unroll
                 for (int h = 0; h < 8; ++h) {
