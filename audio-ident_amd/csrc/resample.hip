@@ -73,17 +73,105 @@ __global__ __launch_bounds__(kResThreads) void k_resample(const float *__restric
     }
 }
 
-static int64_t window_floats(int up, int down, int J) { return (int64_t)(kResBlock - 1) * down / up + J + 2; }
+// MODE 3 (up > 1, the default): phase-major. Outputs m and m + up share a phase, so a thread
+// owns one phase of the block and kResR outputs up apart: it loads its phase's taps once per
+// 8-tap chunk (L1-resident table) and runs kResR dot products with them. Per output that is
+// J input reads from LDS (+ J / kResR tap loads) instead of 2J LDS reads with per-lane phase
+// rows (which also bank-conflicted). Same fma chain per output (taps j = 0..J-1 in order).
+#ifndef AID_RS_PHASE
+#define AID_RS_PHASE 1
+#endif
+#ifndef AID_RS_R
+#define AID_RS_R 16
+#endif
+constexpr int kResR = AID_RS_R;  // outputs per thread (one phase)
+
+template <bool STEREO>
+__global__ __launch_bounds__(256) void k_resample_phase(const float *__restrict__ src, int64_t in_base, int64_t n,
+                                                       int up, int down, int hl, int J,
+                                                       const float *__restrict__ taps, float *__restrict__ dst,
+                                                       int64_t m_first, int64_t m_end) {
+    extern __shared__ float sx[];
+    const int tid = threadIdx.x;
+    const int64_t m0 = m_first + (int64_t)blockIdx.x * up * kResR;
+    const int64_t mlast = min(m0 + (int64_t)up * kResR - 1, m_end - 1);
+    const int64_t lo = (m0 * down + hl) / up - (J - 1);
+    const int64_t hi = (mlast * down + hl) / up;  // inclusive
+    const int cnt = (int)(hi - lo + 1);
+    for (int i = tid; i < cnt; i += blockDim.x) {
+        const int64_t g = lo + i - in_base;
+        float v = 0.0f;
+        if (g >= 0 && g < n) {
+            if constexpr (STEREO) {
+                const float2 s2 = reinterpret_cast<const float2 *>(src)[g];
+                v = (s2.x + s2.y) * 0.5f;
+            } else {
+                v = src[g];
+            }
+        }
+        sx[i] = v;
+    }
+    __syncthreads();
+    for (int t = tid; t < up; t += blockDim.x) {
+        const int64_t c0 = (m0 + t) * down + hl;  // output r: c = c0 + r * up * down
+        const int p = (int)(c0 % up);
+        const int b0 = (int)(c0 / up - lo);       // its input index: b0 + r * down - j
+        const float *tp = taps + (int64_t)p * J;
+        float acc[kResR];
+#pragma unroll
+        for (int r = 0; r < kResR; ++r) acc[r] = 0.0f;
+        for (int jb = 0; jb < J; jb += 8) {
+            float tv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) tv[u] = jb + u < J ? tp[jb + u] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (jb + u >= J) break;  // uniform
+#pragma unroll
+                for (int r = 0; r < kResR; ++r) acc[r] = __builtin_fmaf(tv[u], sx[b0 + r * down - (jb + u)], acc[r]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kResR; ++r) {
+            const int64_t m = m0 + t + (int64_t)r * up;
+            if (m < m_end) dst[m - m_first] = acc[r];
+        }
+    }
+}
+
+// phase-major blocks hold up * kResR outputs: used while that window stays small (common rate
+// pairs: up = 147, 160, 441); very large up (near-coprime rates) keep the 1024-output blocks
+static bool use_phase(int up, int down, int J) {
+    return AID_RS_PHASE && up > 1 && up <= 1024 && ((int64_t)up * kResR - 1) * down / up + J + 2 <= 12288;
+}
+
+static int64_t window_floats(int up, int down, int J) {
+    if (use_phase(up, down, J)) return ((int64_t)up * kResR - 1) * down / up + J + 2;
+    return (int64_t)(kResBlock - 1) * down / up + J + 2;
+}
 
 static bool taps_in_lds(int up, int J) { return up > 1 && (int64_t)up * J <= kResMaxLdsTaps; }
 
 int64_t resample_lds_floats(int up, int down, int J) {
+    if (use_phase(up, down, J)) return window_floats(up, down, J);
     return window_floats(up, down, J) + (taps_in_lds(up, J) ? (((int64_t)up * J + 3) & ~3) : 0);
 }
 
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
                      const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s) {
     if (count <= 0) return;
+    if (use_phase(up, down, J)) {
+        const int64_t per = (int64_t)up * kResR;
+        const dim3 g((unsigned)((count + per - 1) / per)), b((unsigned)std::min(256, (up + 63) / 64 * 64));
+        const size_t lds = (size_t)resample_lds_floats(up, down, J) * sizeof(float);
+        if (channels == 2)
+            hipLaunchKernelGGL((k_resample_phase<true>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst,
+                               m_first, m_first + count);
+        else
+            hipLaunchKernelGGL((k_resample_phase<false>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst,
+                               m_first, m_first + count);
+        return;
+    }
     const dim3 g((unsigned)((count + kResBlock - 1) / kResBlock)), b(kResThreads);
     const size_t lds = (size_t)resample_lds_floats(up, down, J) * sizeof(float);
     const int64_t m_end = m_first + count;

@@ -15,7 +15,7 @@ from aidfp.stream import StreamIdentifier
 
 pytestmark = pytest.mark.gpu
 RATES = [(48000, 16000), (48000, 44100), (44100, 16000), (16000, 48000), (44100, 48000), (22050, 16000),
-         (96000, 44100), (8000, 44100), (16000, 16000)]
+         (96000, 44100), (8000, 44100), (16000, 16000), (44101, 48000)]
 
 
 def _gpu_resample(eng, x, sr_in, sr_out):
