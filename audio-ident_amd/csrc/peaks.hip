@@ -37,6 +37,9 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_PF
 #define AID_K2_PF 4  // prefetch distance in rows (4 or 8): rows it+PF .. are in flight in registers
 #endif
+#ifndef AID_K2_DIAG
+#define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
@@ -75,6 +78,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 #endif
     }
     if (strip >= total_strips) return;
+#if AID_K2_DIAG == 3
+    if (strip >= 0) return;  // launch + strip deal only
+#endif
     int lo = 0, hi = n_clips - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -137,7 +143,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             const int it = base + s;
             if (it >= iters) break;  // workgroup-uniform
             const int buf = (it / kRowsPerStep) & 1;
-            if (s % kRowsPerStep == 0) {
+            if (AID_K2_DIAG != 2 && s % kRowsPerStep == 0) {
                 // stage rows it .. it+3 as keys, then fetch rows it+PF .. (register staging beats
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll
@@ -157,6 +163,30 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 __syncthreads();
             }
             const int r = rbeg + it;
+#if AID_K2_DIAG == 2
+            {
+                // loads only: no LDS staging, no keys
+                const float4 v = pf[s % AID_K2_PF];
+                const int x = __float_as_int(v.x) ^ __float_as_int(v.y) ^ __float_as_int(v.z) ^ __float_as_int(v.w);
+                const uint64_t b0 = __ballot(x == 0x12345);
+                if (r >= t0 && r < t1 && lane < 4) M[(int64_t)r * kMaskWords] = b0;
+                const int rn = rbeg + it + AID_K2_PF;
+                pf[s % AID_K2_PF] = (it + AID_K2_PF < iters && rn >= 0 && rn < F)
+                                        ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+                continue;
+            }
+#endif
+#if AID_K2_DIAG == 1
+            {
+                const int4 me = reinterpret_cast<const int4 *>(rows[buf][s % kRowsPerStep])[tid + 4];
+                const uint64_t b0 = __ballot(me.x > kthr), b1 = __ballot(me.y > kthr), b2 = __ballot(me.z > kthr),
+                               b3 = __ballot(me.w > kthr);
+                if (r >= t0 && r < t1 && lane < 4)
+                    M[(int64_t)r * kMaskWords] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+                continue;
+            }
+#endif
 #if !AID_K2_BLOCKMAX
             const int *rb = rows[buf][s % kRowsPerStep];
 #endif
