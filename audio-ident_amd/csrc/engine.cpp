@@ -49,6 +49,9 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
                                 const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
+int query_lhist_bits();
+void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
+                        const uint32_t *offsets, int64_t *votes, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
@@ -151,6 +154,7 @@ struct aid_engine {
     DevBuf<uint32_t> q_hist;
     DevBuf<int32_t> q_rows, q_nrows;
     DevBuf<uint32_t> q_hot;  // K5h hot-bucket bitmaps, [batch][2^bits / 32]
+    DevBuf<int64_t> q_votes;  // exact votes per query (LDS-histogram eligibility)
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
     DevBuf<float> x_in, x_win;
@@ -185,6 +189,8 @@ struct aid_engine {
     int64_t total_frames = 0, total_strips = 0, total_chunks = 0, total_records = 0;
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
+    bool k5_lhist = true;  // K5a's first attempt counts in LDS (AIDFP_K5_LHIST=0: global histogram only)
+    int64_t k5_lhist_max = 150000;  // ... for queries with at most this many votes (AIDFP_K5_LHIST_MAX)
     int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     size_t k5_batch = 2048;        // global-path queries per launch (AIDFP_K5_BATCH)
@@ -293,6 +299,8 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
+    if (const char *lh = std::getenv("AIDFP_K5_LHIST")) e->k5_lhist = std::atoi(lh) != 0;
+    if (const char *lm = std::getenv("AIDFP_K5_LHIST_MAX")) e->k5_lhist_max = std::atoll(lm);
     if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
@@ -1268,8 +1276,8 @@ int aid_index_load(aid_engine *e, const char *path) {
 }
 
 // run K5 over nq queries whose records are at device ranges (q_start/q_count device arrays).
-// max_recs = the largest query (host-known); the vote histogram gets ~8 buckets per
-// expected vote; queries whose exact LDS table overflowed are re-run with 4x the buckets.
+// Exact per-query vote counts (k_query_votes) choose the path and size the vote histogram;
+// queries whose exact LDS table overflowed are re-run with 4x the buckets. (max_recs is unused.)
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
@@ -1279,22 +1287,33 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     HIP_TRY(e->q_nrows.reserve((size_t)std::max(nq, 1)));
     std::vector<int> todo(nq);
     for (int q = 0; q < nq; ++q) todo[q] = q;
-    std::vector<int64_t> h_start(nq), h_count(nq);
+    std::vector<int64_t> h_start(nq), h_count(nq), h_votes(nq, 0);
     HIP_TRY(hipMemcpyAsync(h_start.data(), qstart_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h_count.data(), qcount_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    {  // exact vote counts: path choice, LDS-histogram eligibility and the global histogram's size
+        HIP_TRY(e->q_votes.reserve((size_t)nq));
+        launch_query_votes(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->q_votes.p, s);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(h_votes.data(), e->q_votes.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
-    if (max_recs < 0)
-        for (int q = 0; q < nq; ++q) max_recs = std::max(max_recs, h_count[q]);
-    const double per_bucket = e->n_buckets_used > 0 ? (double)e->n_indexed / (double)e->n_buckets_used : 1.0;
-    const double votes = std::max(1.0, (double)max_recs * per_bucket);
-    // global histogram: ~2 buckets per expected vote. (Sizing it for the ~10 % of votes that
-    // pass K5a's seen filter measured slower: 20.5k against 27.2k clips/s on config 4.)
-    int bits = 16;
-    while (bits < 24 && (double)(1ull << bits) < 2.0 * votes) ++bits;
+    int64_t vmax = 1;
+    for (int q = 0; q < nq; ++q) vmax = std::max(vmax, h_votes[q]);
+    const double votes = (double)vmax;
+    // global histogram, sized for the votes that pass K5a's 2^20-bit seen filter (all but the
+    // distinct bits: v - m(1 - e^{-v/m})) at ~2 per bucket: a chance bucket reaching
+    // min_match - 1 then has probability ~1e-5. Sizing it for ALL votes (2 buckets each: 2 MB rows on
+    // config 4) spread K5a's random atomics over ~4 GB of rows, all HBM round trips: 16 bits
+    // (256 KB rows, 64 MB for the 256 resident queries: Infinity-Cache resident) took 0.295 s
+    // against 0.383 s for 19 bits on config 4 (37.3k against 28.8k clips/s; 20 bits: 23.4k).
+    const double m_seen = (double)(1 << 20);
+    const double fwd = votes - m_seen * (1.0 - std::exp(-votes / m_seen));
+    int bits = 15;
+    while (bits < 24 && (double)(1ull << bits) < fwd / 2.0) ++bits;
     // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is
     // exact for heavier queries too (overflows fall back; tests/test_gpu_match_load.py) but one
-    // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~180k
-    // votes each) take 48.6 s on it against 1.43 s on the global path
+    // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~540k
+    // votes each) took 48.6 s on it against 1.43 s on the global path
     const bool fast = e->k5_path == 1 || (e->k5_path == 0 && 2.0 * votes <= 65536.0);
     // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
     // through to the global-histogram path below
@@ -1318,19 +1337,32 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();
     }
-    for (int attempt = 1; !todo.empty(); ++attempt, bits += 2) {
-        if (bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
-        const size_t H = (size_t)1 << bits;
-        const int batch = (int)std::max<size_t>(1, std::min<size_t>(e->k5_batch, ((size_t)4 << 30) / (H * 4)));
-        HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
+    // first attempt: LDS histogram (no global row); queries whose exact table overflows go to the
+    // global histogram, then to 4x its buckets per retry
+    bool lh = e->k5_lhist;
+    for (int attempt = 1; !todo.empty(); ++attempt) {
+        if (!lh && bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
+        const int qbits = lh ? query_lhist_bits() : bits;
+        const size_t H = (size_t)1 << qbits;
+        const int batch = lh ? (int)std::max<size_t>(1, e->k5_batch)
+                             : (int)std::max<size_t>(1, std::min<size_t>(e->k5_batch, ((size_t)4 << 30) / (H * 4)));
         HIP_TRY(e->q_hot.reserve((size_t)std::min<int>((int)todo.size(), batch) * (H / 32)));
-        if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5b re-zeroes its rows afterwards
-            HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
-            e->hist_zero_cap = e->q_hist.n;
+        if (!lh) {
+            HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
+            if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5h re-zeroes its rows afterwards
+                HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
+                e->hist_zero_cap = e->q_hist.n;
+            }
         }
         const int64_t *qs = qstart_dev, *qc = qcount_dev;
         int32_t *out_rows = e->q_rows.p, *out_n = e->q_nrows.p;
-        std::vector<int> order = todo;
+        std::vector<int> order, skip;  // skip: too many votes for the LDS histogram
+        for (int q : todo) (lh && h_votes[q] > e->k5_lhist_max ? skip : order).push_back(q);
+        if (order.empty()) {
+            todo.swap(skip);
+            lh = false;
+            continue;
+        }
         if (attempt > 0) {  // gather the overflowed queries' ranges into the scratch arrays' tail
             HIP_TRY(e->x_src.reserve(2 * order.size()));
             std::vector<int64_t> st(order.size()), ct(order.size());
@@ -1350,7 +1382,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             {
                 ProfScope ps(e, AID_K_MATCH, s);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_hist.p, bits, e->q_hot.p, out_rows + (size_t)q0 * mr * 5,
+                             e->cfg.min_match, mr, lh ? nullptr : e->q_hist.p, qbits, e->q_hot.p,
+                             out_rows + (size_t)q0 * mr * 5,
                              out_n + q0, e->tomb_since_build > 0, s);
             }
             HIP_TRY(hipGetLastError());
@@ -1378,7 +1411,10 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             nrows[q] = got_n[i];
             if (rows) std::memcpy(rows + (size_t)q * mr, got.data() + (size_t)i * mr, (size_t)mr * sizeof(aid_match_row));
         }
+        again.insert(again.end(), skip.begin(), skip.end());
         todo.swap(again);
+        if (lh) lh = false;
+        else bits += 2;
     }
     return AID_OK;
 }

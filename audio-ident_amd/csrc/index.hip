@@ -31,6 +31,10 @@ constexpr int kKeyBits = 26;
 constexpr uint32_t kKeys = 1u << kKeyBits;
 constexpr int kVoteCap = 4096;   // LDS (track, d) entries per query
 constexpr int kTrackCap = 1024;  // LDS per-track best entries per query
+// linear-probe bound of the exact (track, d) tables: past it the table counts as overflowed and
+// the query is re-run on more buckets (still exact). Probing a full 4096-slot table per vote had
+// made an overflowing query cost ~100x a normal one.
+constexpr int kProbeMax = 512;
 
 __device__ __forceinline__ uint32_t key26(uint32_t h) {
     return ((h >> 22) << 16) | (((h >> 12) & 0x3FFu) << 6) | (h & 0x3Fu);
@@ -143,9 +147,15 @@ struct QueryParams {
 // (ballot + readlane, scalar loop) -- with U windows' posting loads in flight before use. (One
 // record per wave with lanes over its ~10-200 postings left most lanes idle and serialised
 // recs -> offsets -> post -> tomb round trips per record.)
-template <int U, typename F>
-__device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
-                                              F &&f) {
+// The batch form hands the callback U windows at once (e[u]: posting, tq[u]: query time,
+// ok[u]: a live vote), so K5a can issue its LDS filter tests for all U windows before any of its
+// global atomics: a global atomic counts in vmcnt, and a wait for the next window's posting load
+// would otherwise wait for it too (one L2 round trip per window). The loads are unconditional
+// (invalid lanes read post[0]) so the waits before the windows can count precisely; the record
+// of a window is found with readlane (the record index is wave-uniform), not ds_bpermute.
+template <int U, typename G>
+__device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw,
+                                                    int lane, G &&g) {
     for (int64_t base = (int64_t)wave * 64; base < n; base += (int64_t)nw * 64) {
         const int64_t i = base + lane;
         uint32_t p0 = 0, len = 0;
@@ -168,38 +178,52 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
         for (uint32_t w0 = 0; w0 < total; w0 += 64u * U) {
             uint32_t pos[U];
             int32_t tqs[U];
+            bool ok[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t lo = w0 + 64u * u, j = lo + lane;
-                pos[u] = 0xFFFFFFFFu;
+                pos[u] = 0;
                 tqs[u] = 0;
+                ok[u] = false;
                 if (lo >= total) continue;  // uniform
                 // records whose range [excl, incl) meets [lo, lo + 64): usually 1-2
                 uint64_t m = __ballot(len > 0 && excl < lo + 64u && incl > lo);
                 while (m) {
                     const int rl = __builtin_ctzll(m);
                     m &= m - 1;
-                    const uint32_t e0 = __shfl(excl, rl), e1 = __shfl(incl, rl);
-                    const uint32_t pp = __shfl(p0, rl);
-                    const int32_t tr = __shfl(tq, rl);
+                    const uint32_t e0 = __builtin_amdgcn_readlane(excl, rl), e1 = __builtin_amdgcn_readlane(incl, rl);
+                    const uint32_t pp = __builtin_amdgcn_readlane(p0, rl);
+                    const int32_t tr = __builtin_amdgcn_readlane(tq, rl);
                     if (j >= e0 && j < e1) {
                         pos[u] = pp + (j - e0);
                         tqs[u] = tr;
+                        ok[u] = true;
                     }
                 }
             }
             uint64_t e[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) e[u] = pos[u] != 0xFFFFFFFFu ? qp.post[pos[u]] : 0ull;
+            for (int u = 0; u < U; ++u) e[u] = qp.post[pos[u]];
+            if (qp.tomb_live) {  // uniform
+                uint8_t tb[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (pos[u] == 0xFFFFFFFFu) continue;
-                const uint32_t trk = (uint32_t)e[u];
-                if (qp.tomb_live && qp.tomb[trk]) continue;
-                f(trk, (int32_t)(e[u] >> 32) - tqs[u], tqs[u]);
+                for (int u = 0; u < U; ++u) tb[u] = qp.tomb[(uint32_t)e[u]];
+#pragma unroll
+                for (int u = 0; u < U; ++u) ok[u] = ok[u] && !tb[u];
             }
+            g(e, tqs, ok);
         }
     }
+}
+
+template <int U, typename F>
+__device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
+                                              F &&f) {
+    for_each_vote_batch<U>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u]) f((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u], tqs[u]);
+    });
 }
 
 // one wave per query record; its lanes stride over the record's posting list (coalesced)
@@ -208,6 +232,12 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
 #endif
 #ifndef AID_K5_U
 #define AID_K5_U 16  // 64-posting windows with loads in flight per wave in K5a/K5b (4: 26.9k clips/s, 8: 27.9k, 16: 28.3k)
+#endif
+#ifndef AID_K5_DIAG
+#define AID_K5_DIAG 0  // timing-only K5a variants (wrong results): 1 = no counting, 2 = LDS filter only
+#endif
+#ifndef AID_K5_BLOOM
+#define AID_K5_BLOOM 1  // bits per key in K5a's seen filter (blocked Bloom filter for > 1)
 #endif
 #ifndef AID_K5_SEEN
 #define AID_K5_SEEN 1  // LDS "seen" pre-filter in front of the global histogram (see k_vote_hist)
@@ -227,14 +257,92 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
     __shared__ uint32_t seen[1 << 15];
     for (int i = threadIdx.x; i < (1 << 15); i += blockDim.x) seen[i] = 0u;
     __syncthreads();
+#if AID_K5_DIAG == 1
+    uint32_t acc = 0;  // timing only: enumeration and posting loads, no counting
+    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) { acc ^= mix_td(tr, d); });
+    if (acc == 0x9E3779B1u) H[0] = acc;
+#elif AID_K5_DIAG == 2
     for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
         const uint32_t x = mix_td(tr, d), b = x >> 12, bit = 1u << (b & 31);
-        if (atomicOr(&seen[b >> 5], bit) & bit) atomicAdd(&H[x & hmask], 1u);
+        atomicOr(&seen[b >> 5], bit);  // timing only: the LDS filter without the global histogram
     });
+#elif AID_K5_DIAG == 4
+    uint32_t acc = 0;  // timing only: returning LDS filter, no global histogram
+    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
+        const uint32_t x = mix_td(tr, d), b = x >> 12, bit = 1u << (b & 31);
+        acc += (atomicOr(&seen[b >> 5], bit) & bit) ? 1u : 0u;
+    });
+    if (acc == 0x9E3779B1u) H[0] = acc;
+#elif AID_K5_BLOOM > 1
+    // blocked Bloom filter: the key's AID_K5_BLOOM bits sit in ONE word, so a single atomicOr
+    // tests and sets them together -- of racing votes of one key exactly one sees a bit clear,
+    // and at most the key's first vote is held back (as with one bit). Fewer chance "seen"
+    // collisions reach the global histogram: its random atomics are the kernel's cost.
+    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
+        const uint32_t x = mix_td(tr, d);
+        uint32_t m = (1u << (x & 31)) | (1u << ((x >> 5) & 31));
+        if (AID_K5_BLOOM > 2) m |= 1u << ((x >> 10) & 31);
+        if ((atomicOr(&seen[x >> 17], m) & m) == m) atomicAdd(&H[x & hmask], 1u);
+    });
+#else
+    for_each_vote_batch<AID_K5_U>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
+        uint32_t fw[AID_K5_U];
+#pragma unroll
+        for (int u = 0; u < AID_K5_U; ++u) {  // all U filter tests first (LDS only)
+            const uint32_t x = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]), b = x >> 12;
+            const uint32_t bit = ok[u] ? 1u << (b & 31) : 0u;
+            fw[u] = (atomicOr(&seen[b >> 5], bit) & bit) ? x & hmask : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < AID_K5_U; ++u)  // then the global histogram
+            if (fw[u] != 0xFFFFFFFFu) atomicAdd(&H[fw[u]], 1u);
+    });
+#endif
 #else
     for_each_vote<4>(qp, a, n, wave, nw, lane,
                      [&](uint32_t tr, int32_t d, int32_t) { atomicAdd(&H[mix_td(tr, d) & hmask], 1u); });
 #endif
+}
+
+// K5a, LDS form (the first attempt for every query): the histogram is 2^14 LDS counters
+// next to a 2^19-bit seen filter (64 KB each), so no vote reaches global memory. Sized for the
+// FORWARDED votes -- ~30k of config 4's ~180k votes per window: 1.8 per counter, and a chance
+// bucket reaching min_match - 1 = 11 is ~2e-6 -- it has no 2 MB global row to hit with random
+// atomics (L2 misses, and the true match's ~600 votes serialised on one address: 0.13 of
+// config 4's 0.38 s), and no K5h pass: the hot bitmap row is built from LDS at the end.
+// Same superset rule as k_vote_hist (at most a key's first vote held back), so K5b is unchanged;
+// an overflow of K5b's exact table sends the query to the global path.
+constexpr int kLhBits = 14;
+__global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_lhist(QueryParams qp) {
+    __shared__ uint32_t seen[1 << 14];
+    __shared__ uint32_t cnt[1 << kLhBits];
+    const int q = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int64_t a = qp.qstart[q], n = qp.qcount[q];
+    for (int i = threadIdx.x; i < (1 << 14); i += blockDim.x) {
+        seen[i] = 0u;
+        cnt[i] = 0u;
+    }
+    __syncthreads();
+    for_each_vote_batch<AID_K5_U>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
+        uint32_t fw[AID_K5_U];
+#pragma unroll
+        for (int u = 0; u < AID_K5_U; ++u) {
+            const uint32_t x = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]), b = x >> 13;
+            const uint32_t bit = ok[u] ? 1u << (b & 31) : 0u;
+            fw[u] = (atomicOr(&seen[b >> 5], bit) & bit) ? x & ((1u << kLhBits) - 1) : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < AID_K5_U; ++u)
+            if (fw[u] != 0xFFFFFFFFu) atomicAdd(&cnt[fw[u]], 1u);
+    });
+    __syncthreads();
+    const uint32_t mm = (uint32_t)qp.min_match - 1u;
+    uint64_t *B = reinterpret_cast<uint64_t *>(qp.hot + ((int64_t)q << (kLhBits - 5)));
+    for (int i = threadIdx.x; i < (1 << kLhBits); i += blockDim.x) {
+        const uint64_t m = __ballot(cnt[i] >= mm);
+        if (lane == 0) B[i >> 6] = m;  // i of lane 0 is a multiple of 64
+    }
 }
 
 // K5h: one coalesced pass over each query's histogram row: bucket >= min_match -> a bit of the
@@ -288,6 +396,8 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
         const uint32_t h = mix_td(tr, d);
         const uint32_t hb = h & hmask;
         if (!((hot[hb >> 5] >> (hb & 31)) & 1u)) return;
+        if (AID_K5_DIAG == 3) { atomicAdd(&vcnt[0], 1u); return; }  // timing only: no exact table
+        if (*(volatile int32_t *)&overflow) return;  // the query is re-run on a bigger histogram anyway
         const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
         uint32_t s = (h >> 20) & (kVoteCap - 1);
         int probes = 0;
@@ -299,7 +409,7 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
                 atomicMax(&vmax[s], (uint32_t)tq);
                 break;
             }
-            if (++probes >= kVoteCap) { overflow = 1; break; }
+            if (++probes >= kProbeMax) { overflow = 1; break; }
             s = (s + 1) & (kVoteCap - 1);
         }
     });
@@ -470,7 +580,7 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
                 atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
                 break;
             }
-            if (++probes >= kFastVoteCap) { L.overflow = 1; break; }
+            if (++probes >= kProbeMax) { L.overflow = 1; break; }
             s = (s + 1) & (kFastVoteCap - 1);
         }
     });
@@ -576,9 +686,38 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
                    nrows, tomb_live, hot};
-    hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
-    hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
+    if (!hist) {  // LDS histogram (hist_bits == kLhBits)
+        hipLaunchKernelGGL(k_vote_lhist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
+    } else {
+        hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
+        hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
+    }
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
+}
+
+int query_lhist_bits() { return kLhBits; }
+
+// exact vote count of each query: the sum of its records' bucket lengths (one block per query)
+__global__ __launch_bounds__(256) void k_query_votes(const uint64_t *__restrict__ recs, const int64_t *__restrict__ qstart,
+                                                     const int64_t *__restrict__ qcount,
+                                                     const uint32_t *__restrict__ offsets, int64_t *__restrict__ votes) {
+    __shared__ unsigned long long part[4];
+    const int q = blockIdx.x;
+    const int64_t a = qstart[q], n = qcount[q];
+    unsigned long long v = 0;
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const uint32_t k = key26((uint32_t)recs[a + i]);
+        v += offsets[k + 1] - offsets[k];
+    }
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) votes[q] = (int64_t)(part[0] + part[1] + part[2] + part[3]);
+}
+
+void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
+                        const uint32_t *offsets, int64_t *votes, hipStream_t s) {
+    if (nq > 0) hipLaunchKernelGGL(k_query_votes, dim3(nq), dim3(256), 0, s, recs, qstart, qcount, offsets, votes);
 }
 
 // number of non-empty buckets (for the query histogram sizing)

@@ -67,6 +67,16 @@ __global__ void kW(float4 *__restrict__ p, long n) {
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = make_float4(1.f, 2.f, 3.f, (float)i);
 }
 
+__global__ void kWnt(float4 *__restrict__ p, long n) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    {
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        v4 v = {1.f, 2.f, 3.f, (float)i};
+        __builtin_nontemporal_store(v, reinterpret_cast<v4 *>(p + i));
+    }
+}
+
 int main(int argc, char **argv) {
     const long rows = 219648;  // 256 clips x 858 frames, 4 KB each = 900 MB
     const long n = rows * 256;
@@ -103,6 +113,15 @@ int main(int argc, char **argv) {
             float ms; CK(hipEventElapsedTime(&ms, e0, e1)); tot += ms;
         }
         printf("C W=768 PF4 queued behind W avg %.4f ms (%.2f TB/s)\n", tot / 10, n * 16.0 / (tot / 10) / 1e9);
+        tot = 0; totw = 0;
+        for (int r = 0; r < 10; ++r) {
+            CK(hipEventRecord(e0)); kWnt<<<8192, 256>>>(p, n); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); totw += ms;
+            CK(hipEventRecord(e0)); kB<4, true, false><<<768, 256>>>(p, rows, 768, o); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms, e0, e1)); tot += ms;
+        }
+        printf("Wnt write 900 MB avg %.4f ms; C right after it avg %.4f ms (%.2f TB/s)\n", totw / 10, tot / 10, n * 16.0 / (tot / 10) / 1e9);
+        return 0;
     }
     // chunked write -> read (K1 -> K2 per chunk of clips): reused scratch vs a fresh region per chunk
     for (long mb : {32L, 64L, 112L, 160L, 224L, 300L}) {
