@@ -49,7 +49,6 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
                                 const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
-int query_lhist_bits();
 void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                         const uint32_t *offsets, int64_t *votes, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
@@ -189,8 +188,6 @@ struct aid_engine {
     int64_t total_frames = 0, total_strips = 0, total_chunks = 0, total_records = 0;
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
-    bool k5_lhist = true;  // K5a's first attempt counts in LDS (AIDFP_K5_LHIST=0: global histogram only)
-    int64_t k5_lhist_max = 150000;  // ... for queries with at most this many votes (AIDFP_K5_LHIST_MAX)
     int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     size_t k5_batch = 2048;        // global-path queries per launch (AIDFP_K5_BATCH)
@@ -299,8 +296,6 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
-    if (const char *lh = std::getenv("AIDFP_K5_LHIST")) e->k5_lhist = std::atoi(lh) != 0;
-    if (const char *lm = std::getenv("AIDFP_K5_LHIST_MAX")) e->k5_lhist_max = std::atoll(lm);
     if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
@@ -1280,6 +1275,9 @@ int aid_index_load(aid_engine *e, const char *path) {
 // queries whose exact LDS table overflowed are re-run with 4x the buckets. (max_recs is unused.)
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
+#ifndef AID_K5_PER_BUCKET
+#define AID_K5_PER_BUCKET 2.0  // forwarded votes (1-bit filter estimate) per global histogram bucket
+#endif
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
                        int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
     const int mr = e->cfg.max_results;
@@ -1290,7 +1288,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     std::vector<int64_t> h_start(nq), h_count(nq), h_votes(nq, 0);
     HIP_TRY(hipMemcpyAsync(h_start.data(), qstart_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h_count.data(), qcount_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    {  // exact vote counts: path choice, LDS-histogram eligibility and the global histogram's size
+    {  // exact vote counts: path choice and the global histogram's size
         HIP_TRY(e->q_votes.reserve((size_t)nq));
         launch_query_votes(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->q_votes.p, s);
         HIP_TRY(hipGetLastError());
@@ -1309,7 +1307,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     const double m_seen = (double)(1 << 20);
     const double fwd = votes - m_seen * (1.0 - std::exp(-votes / m_seen));
     int bits = 15;
-    while (bits < 24 && (double)(1ull << bits) < fwd / 2.0) ++bits;
+    while (bits < 24 && (double)(1ull << bits) < fwd / AID_K5_PER_BUCKET) ++bits;
     // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is
     // exact for heavier queries too (overflows fall back; tests/test_gpu_match_load.py) but one
     // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~540k
@@ -1337,32 +1335,19 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();
     }
-    // first attempt: LDS histogram (no global row); queries whose exact table overflows go to the
-    // global histogram, then to 4x its buckets per retry
-    bool lh = e->k5_lhist;
-    for (int attempt = 1; !todo.empty(); ++attempt) {
-        if (!lh && bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
-        const int qbits = lh ? query_lhist_bits() : bits;
-        const size_t H = (size_t)1 << qbits;
-        const int batch = lh ? (int)std::max<size_t>(1, e->k5_batch)
-                             : (int)std::max<size_t>(1, std::min<size_t>(e->k5_batch, ((size_t)4 << 30) / (H * 4)));
+    for (int attempt = 1; !todo.empty(); ++attempt, bits += 2) {
+        if (bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
+        const size_t H = (size_t)1 << bits;
+        const int batch = (int)std::max<size_t>(1, std::min<size_t>(e->k5_batch, ((size_t)4 << 30) / (H * 4)));
+        HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
         HIP_TRY(e->q_hot.reserve((size_t)std::min<int>((int)todo.size(), batch) * (H / 32)));
-        if (!lh) {
-            HIP_TRY(e->q_hist.reserve((size_t)std::min<int>((int)todo.size(), batch) * H));
-            if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5h re-zeroes its rows afterwards
-                HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
-                e->hist_zero_cap = e->q_hist.n;
-            }
+        if (e->hist_zero_cap != e->q_hist.n) {  // fresh allocation; K5h re-zeroes its rows afterwards
+            HIP_TRY(hipMemsetAsync(e->q_hist.p, 0, e->q_hist.n * sizeof(uint32_t), s));
+            e->hist_zero_cap = e->q_hist.n;
         }
         const int64_t *qs = qstart_dev, *qc = qcount_dev;
         int32_t *out_rows = e->q_rows.p, *out_n = e->q_nrows.p;
-        std::vector<int> order, skip;  // skip: too many votes for the LDS histogram
-        for (int q : todo) (lh && h_votes[q] > e->k5_lhist_max ? skip : order).push_back(q);
-        if (order.empty()) {
-            todo.swap(skip);
-            lh = false;
-            continue;
-        }
+        std::vector<int> order = todo;
         if (attempt > 0) {  // gather the overflowed queries' ranges into the scratch arrays' tail
             HIP_TRY(e->x_src.reserve(2 * order.size()));
             std::vector<int64_t> st(order.size()), ct(order.size());
@@ -1382,8 +1367,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             {
                 ProfScope ps(e, AID_K_MATCH, s);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, lh ? nullptr : e->q_hist.p, qbits, e->q_hot.p,
-                             out_rows + (size_t)q0 * mr * 5,
+                             e->cfg.min_match, mr, e->q_hist.p, bits, e->q_hot.p, out_rows + (size_t)q0 * mr * 5,
                              out_n + q0, e->tomb_since_build > 0, s);
             }
             HIP_TRY(hipGetLastError());
@@ -1411,10 +1395,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             nrows[q] = got_n[i];
             if (rows) std::memcpy(rows + (size_t)q * mr, got.data() + (size_t)i * mr, (size_t)mr * sizeof(aid_match_row));
         }
-        again.insert(again.end(), skip.begin(), skip.end());
         todo.swap(again);
-        if (lh) lh = false;
-        else bits += 2;
     }
     return AID_OK;
 }

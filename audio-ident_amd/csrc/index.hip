@@ -237,16 +237,17 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
 #define AID_K5_DIAG 0  // timing-only K5a variants (wrong results): 1 = no counting, 2 = LDS filter only
 #endif
 #ifndef AID_K5_BLOOM
-#define AID_K5_BLOOM 1  // bits per key in K5a's seen filter (blocked Bloom filter for > 1)
+#define AID_K5_BLOOM 2  // bits per key in K5a's seen filter (1 or 2, in one 32-bit word)
 #endif
 #ifndef AID_K5_SEEN
 #define AID_K5_SEEN 1  // LDS "seen" pre-filter in front of the global histogram (see k_vote_hist)
 #endif
-// K5a. With AID_K5_SEEN a vote first sets its key's bit in a 2^20-bit LDS bitmap (128 KB) and
-// reaches the global histogram only if the bit was already set: of a key's c votes at most the
-// first is held back, so a bucket holding a key with c >= min_match votes still counts
-// >= min_match - 1 (K5h tests that). Most chance votes are first occurrences (~180k votes over
-// 2^20 bits: ~8 % collide), so the random global atomics -- the kernel's cost -- drop ~10x.
+// K5a. With AID_K5_SEEN a vote first sets its key's bits in a 2^20-bit LDS "seen" filter (128 KB)
+// and reaches the global histogram only if they were all set already: of a key's c votes at most
+// the first is held back, so a bucket holding a key with c >= min_match votes still counts
+// >= min_match - 1 (K5h tests that). Config 4's windows have ~540k votes each (popular hashes:
+// the vote count is size-biased, ~3x the mean bucket length times the records), and the filter
+// keeps the random global atomics -- the kernel's cost -- to the chance collisions.
 __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams qp) {
     const int q = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -273,25 +274,20 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
         acc += (atomicOr(&seen[b >> 5], bit) & bit) ? 1u : 0u;
     });
     if (acc == 0x9E3779B1u) H[0] = acc;
-#elif AID_K5_BLOOM > 1
-    // blocked Bloom filter: the key's AID_K5_BLOOM bits sit in ONE word, so a single atomicOr
-    // tests and sets them together -- of racing votes of one key exactly one sees a bit clear,
-    // and at most the key's first vote is held back (as with one bit). Fewer chance "seen"
-    // collisions reach the global histogram: its random atomics are the kernel's cost.
-    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
-        const uint32_t x = mix_td(tr, d);
-        uint32_t m = (1u << (x & 31)) | (1u << ((x >> 5) & 31));
-        if (AID_K5_BLOOM > 2) m |= 1u << ((x >> 10) & 31);
-        if ((atomicOr(&seen[x >> 17], m) & m) == m) atomicAdd(&H[x & hmask], 1u);
-    });
 #else
+    // The key's AID_K5_BLOOM bits (a blocked Bloom filter for 2) sit in ONE word, so a single
+    // atomicOr tests and sets them together: of racing votes of one key exactly one sees a bit
+    // clear, so at most the key's first vote is held back, as with one bit. Two bits let fewer
+    // chance "seen" collisions through to the global histogram (config 4: 36.9k -> 39.9k clips/s;
+    // three bits 38.5k).
     for_each_vote_batch<AID_K5_U>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
         uint32_t fw[AID_K5_U];
 #pragma unroll
         for (int u = 0; u < AID_K5_U; ++u) {  // all U filter tests first (LDS only)
-            const uint32_t x = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]), b = x >> 12;
-            const uint32_t bit = ok[u] ? 1u << (b & 31) : 0u;
-            fw[u] = (atomicOr(&seen[b >> 5], bit) & bit) ? x & hmask : 0xFFFFFFFFu;
+            const uint32_t x = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]);
+            uint32_t m = AID_K5_BLOOM > 1 ? (1u << (x & 31)) | (1u << ((x >> 5) & 31)) : 1u << ((x >> 12) & 31);
+            m = ok[u] ? m : 0u;
+            fw[u] = ((atomicOr(&seen[x >> 17], m) & m) == m && m) ? x & hmask : 0xFFFFFFFFu;
         }
 #pragma unroll
         for (int u = 0; u < AID_K5_U; ++u)  // then the global histogram
@@ -302,47 +298,6 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
     for_each_vote<4>(qp, a, n, wave, nw, lane,
                      [&](uint32_t tr, int32_t d, int32_t) { atomicAdd(&H[mix_td(tr, d) & hmask], 1u); });
 #endif
-}
-
-// K5a, LDS form (the first attempt for every query): the histogram is 2^14 LDS counters
-// next to a 2^19-bit seen filter (64 KB each), so no vote reaches global memory. Sized for the
-// FORWARDED votes -- ~30k of config 4's ~180k votes per window: 1.8 per counter, and a chance
-// bucket reaching min_match - 1 = 11 is ~2e-6 -- it has no 2 MB global row to hit with random
-// atomics (L2 misses, and the true match's ~600 votes serialised on one address: 0.13 of
-// config 4's 0.38 s), and no K5h pass: the hot bitmap row is built from LDS at the end.
-// Same superset rule as k_vote_hist (at most a key's first vote held back), so K5b is unchanged;
-// an overflow of K5b's exact table sends the query to the global path.
-constexpr int kLhBits = 14;
-__global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_lhist(QueryParams qp) {
-    __shared__ uint32_t seen[1 << 14];
-    __shared__ uint32_t cnt[1 << kLhBits];
-    const int q = blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int64_t a = qp.qstart[q], n = qp.qcount[q];
-    for (int i = threadIdx.x; i < (1 << 14); i += blockDim.x) {
-        seen[i] = 0u;
-        cnt[i] = 0u;
-    }
-    __syncthreads();
-    for_each_vote_batch<AID_K5_U>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
-        uint32_t fw[AID_K5_U];
-#pragma unroll
-        for (int u = 0; u < AID_K5_U; ++u) {
-            const uint32_t x = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]), b = x >> 13;
-            const uint32_t bit = ok[u] ? 1u << (b & 31) : 0u;
-            fw[u] = (atomicOr(&seen[b >> 5], bit) & bit) ? x & ((1u << kLhBits) - 1) : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int u = 0; u < AID_K5_U; ++u)
-            if (fw[u] != 0xFFFFFFFFu) atomicAdd(&cnt[fw[u]], 1u);
-    });
-    __syncthreads();
-    const uint32_t mm = (uint32_t)qp.min_match - 1u;
-    uint64_t *B = reinterpret_cast<uint64_t *>(qp.hot + ((int64_t)q << (kLhBits - 5)));
-    for (int i = threadIdx.x; i < (1 << kLhBits); i += blockDim.x) {
-        const uint64_t m = __ballot(cnt[i] >= mm);
-        if (lane == 0) B[i >> 6] = m;  // i of lane 0 is a multiple of 64
-    }
 }
 
 // K5h: one coalesced pass over each query's histogram row: bucket >= min_match -> a bit of the
@@ -686,16 +641,10 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
                    nrows, tomb_live, hot};
-    if (!hist) {  // LDS histogram (hist_bits == kLhBits)
-        hipLaunchKernelGGL(k_vote_lhist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
-    } else {
-        hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
-        hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
-    }
+    hipLaunchKernelGGL(k_vote_hist, dim3(nq), dim3(AID_K5_HIST_THREADS), 0, s, qp);
+    hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
-
-int query_lhist_bits() { return kLhBits; }
 
 // exact vote count of each query: the sum of its records' bucket lengths (one block per query)
 __global__ __launch_bounds__(256) void k_query_votes(const uint64_t *__restrict__ recs, const int64_t *__restrict__ qstart,

@@ -1,8 +1,7 @@
 """K5 under heavy vote load (popular hashes, as a 100k-track catalog has them): rows stay
 identical to the CPU oracle (oracle/fp_match.c, FPSPEC 7) on the LDS fast path (forced, up to
 ~10 votes per 16-bit counter; overflows fall back), on the global-histogram path (forced) and
-on the engine's own choice. "global" counts K5a's votes in LDS first (k_vote_lhist);
-"global-hist" forces the global-memory histogram (k_vote_hist + k_hot_scan)."""
+on the engine's own choice."""
 
 import numpy as np
 import pytest
@@ -16,11 +15,10 @@ SR = 44100
 HOP = 512
 
 
-@pytest.mark.parametrize("path", ["auto", "lds", "global", "global-hist"])
+@pytest.mark.parametrize("path", ["auto", "lds", "global"])
 @pytest.mark.parametrize("per_hash", [0, 30, 90, 160])
 def test_rows_equal_oracle_under_load(per_hash, path, monkeypatch):
-    monkeypatch.setenv("AIDFP_K5_PATH", path.split("-")[0])  # read at engine creation
-    monkeypatch.setenv("AIDFP_K5_LHIST", "0" if path == "global-hist" else "1")
+    monkeypatch.setenv("AIDFP_K5_PATH", path)  # read at engine creation
     rng = np.random.default_rng(per_hash)
     track = synth.synth(7, 0, 30 * SR, SR)
     trec = O.fingerprint(track, HOP)
