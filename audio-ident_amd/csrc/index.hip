@@ -175,6 +175,20 @@ __device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64
         }
         const uint32_t excl = incl - len;
         const uint32_t total = __shfl(incl, 63);
+        // the window's record(s) come from a scalar cursor over the 64 records (records average
+        // hundreds of postings, so most windows lie inside one record: one VALU op for the lane's
+        // posting index instead of a ballot + per-record compare/select)
+        int r = 0;
+        uint32_t r_excl = __builtin_amdgcn_readlane(excl, 0), r_incl = __builtin_amdgcn_readlane(incl, 0);
+        uint32_t r_p0 = __builtin_amdgcn_readlane(p0, 0);
+        int32_t r_tq = __builtin_amdgcn_readlane(tq, 0);
+        auto next_rec = [&]() {
+            ++r;
+            r_excl = __builtin_amdgcn_readlane(excl, r);
+            r_incl = __builtin_amdgcn_readlane(incl, r);
+            r_p0 = __builtin_amdgcn_readlane(p0, r);
+            r_tq = __builtin_amdgcn_readlane(tq, r);
+        };
         for (uint32_t w0 = 0; w0 < total; w0 += 64u * U) {
             uint32_t pos[U];
             int32_t tqs[U];
@@ -186,18 +200,20 @@ __device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64
                 tqs[u] = 0;
                 ok[u] = false;
                 if (lo >= total) continue;  // uniform
-                // records whose range [excl, incl) meets [lo, lo + 64): usually 1-2
-                uint64_t m = __ballot(len > 0 && excl < lo + 64u && incl > lo);
-                while (m) {
-                    const int rl = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint32_t e0 = __builtin_amdgcn_readlane(excl, rl), e1 = __builtin_amdgcn_readlane(incl, rl);
-                    const uint32_t pp = __builtin_amdgcn_readlane(p0, rl);
-                    const int32_t tr = __builtin_amdgcn_readlane(tq, rl);
-                    if (j >= e0 && j < e1) {
-                        pos[u] = pp + (j - e0);
-                        tqs[u] = tr;
-                        ok[u] = true;
+                while (r_incl <= lo) next_rec();  // r < 63 here: incl of lane 63 is total > lo
+                if (r_incl >= lo + 64u) {  // the whole window inside record r (uniform)
+                    pos[u] = r_p0 + (j - r_excl);
+                    tqs[u] = r_tq;
+                    ok[u] = true;
+                } else {
+                    for (;;) {  // records r, r+1, ... up to the one holding lo + 63 (or the last)
+                        if (j >= r_excl && j < r_incl) {
+                            pos[u] = r_p0 + (j - r_excl);
+                            tqs[u] = r_tq;
+                            ok[u] = true;
+                        }
+                        if (r_incl >= lo + 64u || r == 63) break;
+                        next_rec();
                     }
                 }
             }
