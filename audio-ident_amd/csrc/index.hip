@@ -35,6 +35,7 @@ constexpr int kTrackCap = 1024;  // LDS per-track best entries per query
 // the query is re-run on more buckets (still exact). Probing a full 4096-slot table per vote had
 // made an overflowing query cost ~100x a normal one.
 constexpr int kProbeMax = 512;
+constexpr int kHotLdsBits = 17;  // K5b stages hot bitmap rows of up to 2^17 bits (16 KB) in LDS
 
 __device__ __forceinline__ uint32_t key26(uint32_t h) {
     return ((h >> 22) << 16) | (((h >> 12) & 0x3FFu) << 6) | (h & 0x3Fu);
@@ -343,6 +344,7 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     __shared__ int32_t out_n;
     __shared__ int32_t overflow;
     __shared__ int32_t rowbuf[kTrackCap][5];
+    __shared__ uint32_t hotl[1 << (kHotLdsBits - 5)];
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
     for (int i = tid; i < kVoteCap; i += blockDim.x) {
@@ -362,11 +364,14 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     const uint32_t *hot = qp.hot + ((int64_t)q << (qp.hist_bits - 5));
     const uint32_t mm = (uint32_t)qp.min_match;
     const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-    // 1. exact table of candidate votes
-    for_each_vote<AID_K5_U>(qp, a, z - a, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
-        const uint32_t h = mix_td(tr, d);
-        const uint32_t hb = h & hmask;
-        if (!((hot[hb >> 5] >> (hb & 31)) & 1u)) return;
+    // 1. exact table of candidate votes. The query's hot bitmap row (2^bits / 32 words) is staged
+    // in LDS while it fits 16 KB (bits <= 17, every first attempt on config 4); all U windows'
+    // bitmap tests run before any table insert
+    const bool hot_in_lds = qp.hist_bits <= kHotLdsBits;
+    if (hot_in_lds)
+        for (int i = tid; i < (1 << (qp.hist_bits - 5)); i += blockDim.x) hotl[i] = hot[i];
+    __syncthreads();
+    auto insert = [&](uint32_t tr, int32_t d, int32_t tq, uint32_t h) {
         if (AID_K5_DIAG == 3) { atomicAdd(&vcnt[0], 1u); return; }  // timing only: no exact table
         if (*(volatile int32_t *)&overflow) return;  // the query is re-run on a bigger histogram anyway
         const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
@@ -383,7 +388,24 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
             if (++probes >= kProbeMax) { overflow = 1; break; }
             s = (s + 1) & (kVoteCap - 1);
         }
-    });
+    };
+    auto phase1 = [&](auto word) {
+        for_each_vote_batch<AID_K5_U>(qp, a, z - a, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
+            uint32_t h[AID_K5_U];
+            bool hit[AID_K5_U];
+#pragma unroll
+            for (int u = 0; u < AID_K5_U; ++u) {
+                h[u] = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]);
+                const uint32_t hb = h[u] & hmask;
+                hit[u] = ok[u] && ((word(hb >> 5) >> (hb & 31)) & 1u);
+            }
+#pragma unroll
+            for (int u = 0; u < AID_K5_U; ++u)
+                if (hit[u]) insert((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u], tqs[u], h[u]);
+        });
+    };
+    if (hot_in_lds) phase1([&](uint32_t w) { return hotl[w]; });
+    else phase1([&](uint32_t w) { return hot[w]; });
     __syncthreads();
     // 2. best d per track: max count, then smallest d
     for (int s = tid; s < kVoteCap; s += blockDim.x) {
