@@ -54,7 +54,7 @@ void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
-                  hipStream_t s);
+                  int parts, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
@@ -189,6 +189,7 @@ struct aid_engine {
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
     int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
+    int k5_parts = 0;      // AIDFP_K5_PARTS: K5a key partitions per query (0 = by vote count)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     size_t k5_batch = 2048;        // global-path queries per launch (AIDFP_K5_BATCH)
     hipStream_t last_stream = nullptr;
@@ -296,6 +297,10 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
+    if (const char *kp = std::getenv("AIDFP_K5_PARTS")) {  // 1, 2 or 4 (0 = by vote count)
+        const int v = std::atoi(kp);
+        e->k5_parts = v >= 4 ? 4 : v >= 2 ? 2 : v >= 1 ? 1 : 0;
+    }
     if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
@@ -1304,8 +1309,11 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // config 4) spread K5a's random atomics over ~4 GB of rows, all HBM round trips: 16 bits
     // (256 KB rows, 64 MB for the 256 resident queries: Infinity-Cache resident) took 0.295 s
     // against 0.383 s for 19 bits on config 4 (37.3k against 28.8k clips/s; 20 bits: 23.4k).
-    const double m_seen = (double)(1 << 20);
-    const double fwd = votes - m_seen * (1.0 - std::exp(-votes / m_seen));
+    // K5a key partitions (a workgroup and a 2^20-bit seen filter each): two once the filter
+    // saturates (> 2^18 votes; config 4's ~540k: 46.6k -> 60.2k clips/s), else one
+    const int parts = e->k5_parts > 0 ? e->k5_parts : votes > (double)(1 << 18) ? 2 : 1;
+    const double m_seen = (double)(1 << 20), vp = votes / parts;
+    const double fwd = parts * (vp - m_seen * (1.0 - std::exp(-vp / m_seen)));
     int bits = 15;
     while (bits < 24 && (double)(1ull << bits) < fwd / AID_K5_PER_BUCKET) ++bits;
     // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is
@@ -1368,7 +1376,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
                 ProfScope ps(e, AID_K_MATCH, s);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_hist.p, bits, e->q_hot.p, out_rows + (size_t)q0 * mr * 5,
-                             out_n + q0, e->tomb_since_build > 0, s);
+                             out_n + q0, e->tomb_since_build > 0, parts, s);
             }
             HIP_TRY(hipGetLastError());
         }

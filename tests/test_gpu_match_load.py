@@ -1,7 +1,8 @@
 """K5 under heavy vote load (popular hashes, as a 100k-track catalog has them): rows stay
 identical to the CPU oracle (oracle/fp_match.c, FPSPEC 7) on the LDS fast path (forced, up to
 ~10 votes per 16-bit counter; overflows fall back), on the global-histogram path (forced) and
-on the engine's own choice."""
+on the engine's own choice. "global2" splits K5a's keys over two workgroups per query (the
+engine's choice above 2^18 votes)."""
 
 import numpy as np
 import pytest
@@ -15,10 +16,11 @@ SR = 44100
 HOP = 512
 
 
-@pytest.mark.parametrize("path", ["auto", "lds", "global"])
+@pytest.mark.parametrize("path", ["auto", "lds", "global", "global2"])
 @pytest.mark.parametrize("per_hash", [0, 30, 90, 160])
 def test_rows_equal_oracle_under_load(per_hash, path, monkeypatch):
-    monkeypatch.setenv("AIDFP_K5_PATH", path)  # read at engine creation
+    monkeypatch.setenv("AIDFP_K5_PATH", path.rstrip("2"))  # read at engine creation
+    monkeypatch.setenv("AIDFP_K5_PARTS", "2" if path == "global2" else "0")
     rng = np.random.default_rng(per_hash)
     track = synth.synth(7, 0, 30 * SR, SR)
     trec = O.fingerprint(track, HOP)
