@@ -24,10 +24,10 @@
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       hipStream_t s);
+                       uint32_t *hot, float thr, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
-                      uint64_t *mask, hipStream_t s);
+                      const uint32_t *hot, uint64_t *mask, hipStream_t s);
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
@@ -127,6 +127,7 @@ struct aid_engine {
     DevBuf<float> pcm_stage;
     DevBuf<float> power;
     DevBuf<uint64_t> mask;
+    DevBuf<uint32_t> hotw;  // K1 -> K2: per power row, bit b = 64-bin block b has a value > thr
     DevBuf<ClipDesc> desc;
     DevBuf<int64_t> chunk_counts;
     DevBuf<uint64_t> records;
@@ -482,6 +483,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     HIP_TRY(e->desc.reserve((size_t)n_clips + 1));
     HIP_TRY(e->power.reserve((size_t)frames * kBins));
     HIP_TRY(e->mask.reserve((size_t)frames * kMaskWords));
+    HIP_TRY(e->hotw.reserve((size_t)frames + 1));
     HIP_TRY(e->chunk_counts.reserve((size_t)chunks + 1));
     HIP_TRY(e->records.reserve((size_t)recs + 1));
     HIP_TRY(e->counts.reserve((size_t)n_clips + 1));
@@ -518,7 +520,8 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     if (frames > 0) {
         {
             ProfScope ps(e, AID_K_STFT, s);
-            launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false, s);
+            launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false,
+                              e->hotw.p, e->cfg.peak_threshold, s);
         }
         if (loc == AID_PCM_HOST) {
             if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
@@ -527,7 +530,8 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         }
         {
             ProfScope ps(e, AID_K_PEAKS, s);
-            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->mask.p, s);
+            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
+                             e->mask.p, s);
         }
         if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s);
@@ -638,7 +642,7 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
         launch_stft_power(d_pcm, d_desc, 1, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
-                          d_out, true, s);
+                          d_out, true, nullptr, e->cfg.peak_threshold, s);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);

@@ -57,7 +57,7 @@ __device__ __forceinline__ int pkey(float x) {
 
 __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
-                                                  uint64_t *__restrict__ mask) {
+                                                  const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask) {
     __shared__ __attribute__((aligned(16))) int rows[2][kRowsPerStep][kBins + 32];
 #if AID_K2_BLOCKMAX
     __shared__ __attribute__((aligned(16))) int bms[2][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
@@ -129,13 +129,22 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
     const int rbeg = t0 - kPeakDT;
     const int iters = (t1 - t0) + 2 * kPeakDT;
+    // K1's hot-block word of each row: a thread loads its 4 bins only if their 64-bin block has a
+    // value > thr; others stay 0 (a value <= thr neither is a peak nor suppresses one: exact).
+    // Words are fetched one step ahead of the row loads they gate (scalar loads)
+    const uint32_t *HW = hot + fb;
+    const int myb = tid >> 4;
+    auto hotword = [&](int r) -> uint32_t { return (r >= 0 && r < F) ? HW[r] : 0u; };
     float4 pf[AID_K2_PF];  // rows of the next batch(es), in flight
 #pragma unroll
     for (int j = 0; j < AID_K2_PF; ++j) {
         const int r = rbeg + j;
-        pf[j] = (j < iters && r >= 0 && r < F) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
-                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        pf[j] = (j < iters && ((hotword(r) >> myb) & 1u)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
+                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    uint32_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
+#pragma unroll
+    for (int j = 0; j < kRowsPerStep; ++j) hw[j] = hotword(rbeg + AID_K2_PF + j);
 
     for (int base = 0; base < iters; base += 8) {
 #pragma unroll
@@ -156,9 +165,10 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                     bms[buf][j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
 #endif
                     const int rn = rbeg + it + j + AID_K2_PF;
-                    pf[slot] = (it + j + AID_K2_PF < iters && rn >= 0 && rn < F)
+                    pf[slot] = (it + j + AID_K2_PF < iters && ((hw[j] >> myb) & 1u))
                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+                    hw[j] = hotword(rn + kRowsPerStep);
                 }
                 __syncthreads();
             }
@@ -272,10 +282,10 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 }
 
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
-                      float thr, uint64_t *mask, hipStream_t s) {
+                      float thr, const uint32_t *hot, uint64_t *mask, hipStream_t s) {
     if (total_strips <= 0) return;
     hipLaunchKernelGGL(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
-                       strip_len, thr, mask);
+                       strip_len, thr, hot, mask);
 }
 
 // resident K2 workgroups per CU (registers / LDS), for sizing strips to one round

@@ -90,7 +90,8 @@ template <bool LOGMAG, int ROWS>
 __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
                                                                 int64_t total, int64_t n_waves,
-                                                                const Tables *__restrict__ tab, float *__restrict__ out) {
+                                                                const Tables *__restrict__ tab, float *__restrict__ out,
+                                                                uint32_t *__restrict__ hot, float thr) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
@@ -178,6 +179,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
     const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + lane;
     float *dst = out + (clips[lo].frame_base + t0) * kBins;
+    uint32_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
 
     float2 ring[16];
 #pragma unroll
@@ -340,6 +342,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
                 wave_lds_sync();
                 float *drow = dst + (int64_t)f * kBins;
+                // hot blocks of the row: bit b = some bin of 64-bin block b is > thr (K2 skips the
+                // others: a value <= thr can neither be a peak nor suppress one, FPSPEC 5)
+                uint32_t hotw = 0;
                 float acc10 = 0.f;
                 float pv11[16];  // AID_K1_DIAG 11: the lane's 16 powers, stored as 4 dwordx4 (timing only)
                 // real split, bins in mirror pairs (k, 1024-k): one read of Z[k], Z[1024-k] serves
@@ -377,7 +382,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         else if (AID_K1_DIAG == 10) acc10 += P;
                         else if (AID_K1_DIAG == 11) pv11[2 * i] = P;
                         else drow[k] = P;
+                        if constexpr (!LOGMAG) hotw |= __ballot(P > thr) ? 1u << i : 0u;  // bins 64i..64i+63
                     }
+                    bool hot2 = false;
                     if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
                         const float2 tw = cmul(make_float2(orr, -oi), make_float2(t2.z, t2.w));
                         const float xr = er + tw.x, xi = -ei + tw.y;
@@ -386,8 +393,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         else if (AID_K1_DIAG == 10) acc10 += P;
                         else if (AID_K1_DIAG == 11) pv11[2 * i + 1] = P;
                         else drow[1024 - k] = P;
+                        hot2 = P > thr;
                     } else if (AID_K1_DIAG == 11) {
                         pv11[2 * i + 1] = 0.f;
+                    }
+                    if constexpr (!LOGMAG) {  // lanes 1..63: bins of block 15 - i; lane 0 (i > 0): block 16 - i
+                        const uint64_t hb = __ballot(hot2);
+                        hotw |= (hb >> 1) ? 1u << (15 - i) : 0u;
+                        hotw |= (hb & 1) ? 1u << (16 - i) : 0u;
                     }
                 }
                 if (AID_K1_DIAG == 10) drow[lane] = acc10;
@@ -405,6 +418,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
                     if constexpr (LOGMAG) drow[512] = 10.0f * log10f(P + 1e-10f);
                     else drow[512] = P;
+                    if (P > thr) hotw |= 1u << 8;
+                }
+                if constexpr (!LOGMAG) {
+                    hotw = __builtin_amdgcn_readlane(hotw, 0);  // lane 0 also holds bin 512's bit
+                    if (lane == 0) dhot[f] = hotw;
                 }
                 wave_lds_sync();
             }
@@ -418,13 +436,13 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 
 template <bool LOGMAG>
 static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
-                        int64_t total, int64_t n_waves, const Tables *tab, float *out) {
+                        int64_t total, int64_t n_waves, const Tables *tab, float *out, uint32_t *hot, float thr) {
     switch (rows) {
-        case 1: hipLaunchKernelGGL((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
-        case 2: hipLaunchKernelGGL((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
-        case 4: hipLaunchKernelGGL((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
-        case 8: hipLaunchKernelGGL((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
-        default: hipLaunchKernelGGL((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out); break;
+        case 1: hipLaunchKernelGGL((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 2: hipLaunchKernelGGL((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 4: hipLaunchKernelGGL((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 8: hipLaunchKernelGGL((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        default: hipLaunchKernelGGL((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
     }
 }
 
@@ -432,7 +450,7 @@ static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pc
 // slots = resident K1 waves on the device (CUs x kStftWaves)
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       hipStream_t s) {
+                       uint32_t *hot, float thr, hipStream_t s) {
     if (total_frames <= 0) return;
 #if AID_K1_BALANCED
     // one round of equal ranges; at least kStftStrip frames per wave (a ring fill per segment)
@@ -443,8 +461,8 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
     (void)slots;
 #endif
     const dim3 g((unsigned)((n_waves + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
-    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out);
-    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out);
+    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr);
+    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr);
 }
 
 }  // namespace aid
