@@ -37,6 +37,9 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_PF
 #define AID_K2_PF 4  // prefetch distance in rows (4 or 8): rows it+PF .. are in flight in registers
 #endif
+#ifndef AID_K2_COLDSKIP
+#define AID_K2_COLDSKIP 1  // a wave whose +-15-bin neighbourhood is all cold in a row takes a short path
+#endif
 #ifndef AID_K2_DIAG
 #define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
 #endif
@@ -145,6 +148,13 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     uint32_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) hw[j] = hotword(rbeg + AID_K2_PF + j);
+    // hot words of the rows in flight (hsave) and of the rows being processed (hcur)
+    static_assert(!AID_K2_COLDSKIP || AID_K2_PF == kRowsPerStep, "cold skip tracks rows one step ahead");
+    uint32_t hsave[kRowsPerStep], hcur[kRowsPerStep];
+#pragma unroll
+    for (int j = 0; j < kRowsPerStep; ++j) hsave[j] = hcur[j] = hotword(rbeg + j);
+    // blocks 4w-1 .. 4w+4 hold the wave's bins and their +-15 neighbours
+    const uint32_t wmask = (0x3Fu << (4 * wave)) >> 1;
 
     for (int base = 0; base < iters; base += 8) {
 #pragma unroll
@@ -165,6 +175,8 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                     bms[buf][j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
 #endif
                     const int rn = rbeg + it + j + AID_K2_PF;
+                    hcur[j] = hsave[j];
+                    hsave[j] = hw[j];
                     pf[slot] = (it + j + AID_K2_PF < iters && ((hw[j] >> myb) & 1u))
                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -197,6 +209,21 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 continue;
             }
 #endif
+            bool pk[4];
+            if (AID_K2_COLDSKIP && !(hcur[s % kRowsPerStep] & wmask)) {
+                // every key the wave's windows see is 0: fm = 0, no candidate (p = 0 is never > the
+                // threshold); only the vertical ring advances and row r-7 is decided
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int m2 = fprev[i];
+                    fprev[i] = 0;
+                    m2r[s][i] = m2;
+                    const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
+                    m7p[i] = m7;
+                    pk[i] = pend[(s + 1) & 7][i] >= m7;
+                    pend[s][i] = -1;
+                }
+            } else {
 #if !AID_K2_BLOCKMAX
             const int *rb = rows[buf][s % kRowsPerStep];
 #endif
@@ -254,7 +281,6 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 
             // candidates only inside the strip's output rows (uniform): other rows get +inf
             const int thr_row = (r >= t0 && r < t1) ? kthr : kInf;
-            bool pk[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int p = q[16 + i];
@@ -270,6 +296,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 // row r-7 (slot s+1) has now met all 7 later rows: p >= their row-max
                 pk[i] = pend[(s + 1) & 7][i] >= m7;
                 pend[s][i] = (c1 >= R[i]) ? c1 : -1;
+            }
             }
             const uint64_t b0 = __ballot(pk[0]), b1 = __ballot(pk[1]), b2 = __ballot(pk[2]), b3 = __ballot(pk[3]);
             const int rd = r - kPeakDT;
