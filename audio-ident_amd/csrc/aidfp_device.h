@@ -3,12 +3,31 @@
 // Every expression here is the binary32 op sequence FPSPEC 3-4 pins; the build
 // uses -ffp-contract=off so hipcc emits exactly one v_mul/v_add/v_fma per op.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "aidfp_layout.h"
 
 namespace aid {
+
+// Launch-attached timing (hipExtLaunchKernel): the engine's profiler hands the next launch on this
+// thread a start/stop event pair, and the runtime stamps them from the dispatch packet itself. No
+// marker packets go between the extraction kernels, so K1 -> K2 -> K3 run back to back while timed
+// (hipEventRecord markers cost ~5 us each plus a cache release between every pair of kernels).
+struct LaunchTiming {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+inline LaunchTiming &launch_timing() {
+    static thread_local LaunchTiming t;
+    return t;
+}
+template <typename... Args, typename F = void (*)(Args...)>
+inline void timed_launch(F kernel, dim3 g, dim3 b, uint32_t shm, hipStream_t s, Args... args) {
+    LaunchTiming &t = launch_timing();
+    hipExtLaunchKernelGGL(kernel, g, b, shm, s, t.start, t.stop, 0u, args...);
+    t.start = t.stop = nullptr;
+}
 
 struct Tables {
     float2 win2[1024];  // (w[2m], w[2m+1])

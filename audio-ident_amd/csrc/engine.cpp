@@ -215,19 +215,42 @@ static hipEvent_t take_event(aid_engine *e) {
     return ev;
 }
 
+// attached = the scope wraps exactly one timed_launch: its events are stamped by the dispatch itself
+// (aidfp_device.h LaunchTiming); otherwise two hipEventRecord markers bracket the scope.
 struct ProfScope {
     aid_engine *e;
     int k;
     hipStream_t s;
-    hipEvent_t a = nullptr;
-    ProfScope(aid_engine *e_, int k_, hipStream_t s_) : e(e_), k(k_), s(s_) {
-        if (e->profiling && (a = take_event(e))) (void)hipEventRecord(a, s);
+    bool attached;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(aid_engine *e_, int k_, hipStream_t s_, bool attached_ = false) : e(e_), k(k_), s(s_), attached(attached_) {
+        if (!e->profiling || !(a = take_event(e))) return;
+        if (!attached) {
+            (void)hipEventRecord(a, s);
+            return;
+        }
+        if (!(b = take_event(e))) {
+            e->pool.push_back(a);
+            a = nullptr;
+            return;
+        }
+        launch_timing().start = a;
+        launch_timing().stop = b;
     }
     ~ProfScope() {
         if (!a) return;
-        hipEvent_t b = take_event(e);
-        if (!b) return;
-        (void)hipEventRecord(b, s);
+        if (attached) {
+            LaunchTiming &t = launch_timing();
+            if (t.start) {  // nothing was launched: the events were never stamped
+                t.start = t.stop = nullptr;
+                e->pool.push_back(a);
+                e->pool.push_back(b);
+                return;
+            }
+        } else {
+            if (!(b = take_event(e))) return;
+            (void)hipEventRecord(b, s);
+        }
         e->pending.push_back({k, a, b});
     }
 };
@@ -519,7 +542,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     e->total_records = recs;
     if (frames > 0) {
         {
-            ProfScope ps(e, AID_K_STFT, s);
+            ProfScope ps(e, AID_K_STFT, s, true);
             launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false,
                               e->hotw.p, e->cfg.peak_threshold, s);
         }
@@ -529,17 +552,17 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
             e->stage_ev_live = true;
         }
         {
-            ProfScope ps(e, AID_K_PEAKS, s);
+            ProfScope ps(e, AID_K_PEAKS, s, true);
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
                              e->mask.p, s);
         }
         if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
-            ProfScope ps(e, AID_K_LANDMARK_COUNT, s);
+            ProfScope ps(e, AID_K_LANDMARK_COUNT, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
                              false, s);
         }
         {
-            ProfScope ps(e, AID_K_LANDMARK_WRITE, s);
+            ProfScope ps(e, AID_K_LANDMARK_WRITE, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
                              true, s);
         }

@@ -193,10 +193,10 @@ void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, 
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s) {
     if (total_chunks <= 0) return;
     if (write)
-        hipLaunchKernelGGL(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
+        timed_launch(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
                            total_chunks, chunk_counts, records, clip_counts);
     else
-        hipLaunchKernelGGL(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
+        timed_launch(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
                            total_chunks, chunk_counts, records, clip_counts);
 }
 

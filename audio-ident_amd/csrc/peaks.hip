@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
                       float thr, const uint32_t *hot, uint64_t *mask, hipStream_t s) {
     if (total_strips <= 0) return;
-    hipLaunchKernelGGL(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
+    timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
                        strip_len, thr, hot, mask);
 }
 

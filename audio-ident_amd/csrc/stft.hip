@@ -438,11 +438,11 @@ template <bool LOGMAG>
 static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
                         int64_t total, int64_t n_waves, const Tables *tab, float *out, uint32_t *hot, float thr) {
     switch (rows) {
-        case 1: hipLaunchKernelGGL((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        case 2: hipLaunchKernelGGL((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        case 4: hipLaunchKernelGGL((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        case 8: hipLaunchKernelGGL((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        default: hipLaunchKernelGGL((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
     }
 }
 
