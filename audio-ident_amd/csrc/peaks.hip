@@ -40,6 +40,9 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_COLDSKIP
 #define AID_K2_COLDSKIP 1  // a wave whose +-15-bin neighbourhood is all cold in a row takes a short path
 #endif
+#ifndef AID_K2_ROT
+#define AID_K2_ROT 1  // rotate the wave -> bin-quarter map by blockIdx (SIMD load balance)
+#endif
 #ifndef AID_K2_DIAG
 #define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
 #endif
@@ -65,9 +68,13 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 #if AID_K2_BLOCKMAX
     __shared__ __attribute__((aligned(16))) int bms[2][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
 #endif
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
+    // wave = the 256-bin quarter of the row this wave owns, rotated by the workgroup index: the
+    // waves of a workgroup go to the CU's 4 SIMDs in order, so without rotation every workgroup's
+    // low-frequency (hot) quarter lands on SIMD 0 and its cold top quarter on SIMD 3
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(AID_K2_ROT ? (((int)(threadIdx.x >> 6) + (int)blockIdx.x) & 3)
+                                                               : (int)(threadIdx.x >> 6));
+    const int tid = wave * 64 + lane;  // owner of bins 4 tid .. 4 tid + 3
     constexpr int kInf = 0x7F800000;  // key of +inf
 
     // XCD-aware deal: consecutive strips -> blocks b, b+8, b+16 ... (one XCD's L2)
