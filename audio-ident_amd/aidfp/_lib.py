@@ -19,6 +19,7 @@ AID_ERR_NOMEM = -3
 AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
+AID_FLAG_KEEP_POWER = 1
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
 AID_K_COUNT = 8
 KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample",
@@ -43,7 +44,8 @@ class AidConfig(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("min_match", ctypes.c_int32),
         ("max_results", ctypes.c_int32),
-        ("reserved", ctypes.c_int32 * 10),
+        ("flags", ctypes.c_int32),
+        ("reserved", ctypes.c_int32 * 9),
     ]
 
 

@@ -26,7 +26,7 @@ def _p(a: np.ndarray) -> ctypes.c_void_p:
 
 class Engine:
     def __init__(self, sample_rate: int, hop: int = 0, peak_threshold: float = 0.0, device: int = -1,
-                 min_match: int = 0, max_results: int = 0):
+                 min_match: int = 0, max_results: int = 0, keep_power: bool = False):
         lib = L.load()
         cfg = AidConfig()
         check(lib.aid_config_default(int(sample_rate), ctypes.byref(cfg)))
@@ -39,6 +39,8 @@ class Engine:
             cfg.min_match = min_match
         if max_results:
             cfg.max_results = max_results
+        if keep_power:  # parity/debug: the whole power plane for power() (K1 otherwise skips cold blocks)
+            cfg.flags |= L.AID_FLAG_KEEP_POWER
         h = ctypes.c_void_p()
         rc = lib.aid_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc == AID_ERR_DEVICE:

@@ -24,7 +24,7 @@
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, hipStream_t s);
+                       uint32_t *hot, float thr, bool keep_power, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
                       const uint32_t *hot, uint64_t *mask, hipStream_t s);
@@ -303,6 +303,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     if (!(c.peak_threshold > 0.0f)) return fail(AID_ERR_INVALID, "peak_threshold must be > 0");
     if (c.min_match <= 0) c.min_match = 12;
     if (c.max_results <= 0) c.max_results = 50;
+    if (c.flags & ~AID_FLAG_KEEP_POWER) return fail(AID_ERR_INVALID, "unknown aid_config.flags bits");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (ndev <= 0) return fail(AID_ERR_DEVICE, "no HIP device visible");
@@ -328,7 +329,9 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
-    hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
+    // blocking stream: ordered against the legacy default stream (torch's default), so device
+    // buffers the caller filled there without a stream handle are complete before NULL-stream calls
+    hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamDefault);
     if (he != hipSuccess) {
         delete e;
         return fail(AID_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(he));
@@ -544,7 +547,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         {
             ProfScope ps(e, AID_K_STFT, s, true);
             launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false,
-                              e->hotw.p, e->cfg.peak_threshold, s);
+                              e->hotw.p, e->cfg.peak_threshold, (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0, s);
         }
         if (loc == AID_PCM_HOST) {
             if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
@@ -619,6 +622,8 @@ int aid_result_power(aid_engine *e, int32_t clip, float *out, int64_t cap) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     if (!e->have_result) return fail(AID_ERR_STATE, "no extraction yet");
     if (clip < 0 || clip >= e->n_clips) return fail(AID_ERR_INVALID, "clip index out of range");
+    if (!(e->cfg.flags & AID_FLAG_KEEP_POWER))
+        return fail(AID_ERR_STATE, "aid_result_power: engine created without AID_FLAG_KEEP_POWER (cold blocks not stored)");
     const int64_t F = e->clip_frames[clip];
     if (F * kBins > cap) return fail(AID_ERR_INVALID, "output capacity too small");
     if (int rc = aid_sync(e)) return rc;
@@ -665,7 +670,7 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
         launch_stft_power(d_pcm, d_desc, 1, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
-                          d_out, true, nullptr, e->cfg.peak_threshold, s);
+                          d_out, true, nullptr, e->cfg.peak_threshold, true, s);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);

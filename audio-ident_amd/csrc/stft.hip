@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
                                                                 int64_t total, int64_t n_waves,
                                                                 const Tables *__restrict__ tab, float *__restrict__ out,
-                                                                uint32_t *__restrict__ hot, float thr) {
+                                                                uint32_t *__restrict__ hot, float thr, int keep) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
@@ -346,6 +346,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 // others: a value <= thr can neither be a peak nor suppress one, FPSPEC 5)
                 uint32_t hotw = 0;
                 float acc10 = 0.f;
+                float pm[8];  // the mirror bins 1024-k, held until hotw is complete
                 float pv11[16];  // AID_K1_DIAG 11: the lane's 16 powers, stored as 4 dwordx4 (timing only)
                 // real split, bins in mirror pairs (k, 1024-k): one read of Z[k], Z[1024-k] serves
                 // both. For bin 1024-k the FPSPEC sums are the same exact values with signs
@@ -378,11 +379,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float2 tw = cmul(make_float2(orr, oi), make_float2(t2.x, t2.y));
                         const float xr = er + tw.x, xi = ei + tw.y;
                         const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                        const uint64_t hd = LOGMAG ? 0 : __ballot(P > thr);
                         if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
                         else if (AID_K1_DIAG == 10) acc10 += P;
                         else if (AID_K1_DIAG == 11) pv11[2 * i] = P;
-                        else drow[k] = P;
-                        if constexpr (!LOGMAG) hotw |= __ballot(P > thr) ? 1u << i : 0u;  // bins 64i..64i+63
+                        else if (keep || hd) drow[k] = P;  // block i exactly
+                        if constexpr (!LOGMAG) hotw |= hd ? 1u << i : 0u;  // bins 64i..64i+63
                     }
                     bool hot2 = false;
                     if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
@@ -392,6 +394,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         if constexpr (LOGMAG) drow[1024 - k] = 10.0f * log10f(P + 1e-10f);
                         else if (AID_K1_DIAG == 10) acc10 += P;
                         else if (AID_K1_DIAG == 11) pv11[2 * i + 1] = P;
+                        else if (!LOGMAG) pm[i] = P;  // stored once the row's hot word is known
                         else drow[1024 - k] = P;
                         hot2 = P > thr;
                     } else if (AID_K1_DIAG == 11) {
@@ -423,6 +426,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 if constexpr (!LOGMAG) {
                     hotw = __builtin_amdgcn_readlane(hotw, 0);  // lane 0 also holds bin 512's bit
                     if (lane == 0) dhot[f] = hotw;
+                    // mirror store i covers bins 1025-64(i+1) .. 1023-64i of block 15-i (lanes 1..63)
+                    // and bin 1024-64i of block 16-i (lane 0): written when either block is hot. A
+                    // skipped store leaves only bins of cold blocks stale, which K2 never reads.
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t need = (hotw >> (15 - i)) | (i > 0 ? hotw >> (16 - i) : 0u);
+                        if ((keep || (need & 1u)) && (i > 0 || lane != 0)) drow[1024 - (lane + 64 * i)] = pm[i];
+                    }
                 }
                 wave_lds_sync();
             }
@@ -436,13 +447,13 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 
 template <bool LOGMAG>
 static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
-                        int64_t total, int64_t n_waves, const Tables *tab, float *out, uint32_t *hot, float thr) {
+                        int64_t total, int64_t n_waves, const Tables *tab, float *out, uint32_t *hot, float thr, int keep) {
     switch (rows) {
-        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
-        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr); break;
+        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
+        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
+        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
+        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
+        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
     }
 }
 
@@ -450,7 +461,7 @@ static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pc
 // slots = resident K1 waves on the device (CUs x kStftWaves)
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, hipStream_t s) {
+                       uint32_t *hot, float thr, bool keep_power, hipStream_t s) {
     if (total_frames <= 0) return;
 #if AID_K1_BALANCED
     // one round of equal ranges; at least kStftStrip frames per wave (a ring fill per segment)
@@ -461,8 +472,8 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
     (void)slots;
 #endif
     const dim3 g((unsigned)((n_waves + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
-    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr);
-    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr);
+    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr, 1);
+    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep_power ? 1 : 0);
 }
 
 }  // namespace aid

@@ -11,7 +11,9 @@
  * Conventions: every function returns AID_OK (0) or a negative AID_ERR_*;
  * aid_last_error() returns a thread-local message for the last failure. Pointers
  * are plain host or device pointers as documented per call; `stream` is a
- * hipStream_t passed as void* (NULL = the engine's own stream). An engine is
+ * hipStream_t passed as void* (NULL = the engine's own stream, a blocking stream:
+ * it is ordered after work the caller queued on the legacy default stream, so
+ * buffers produced there are complete before the engine reads them). An engine is
  * bound to one GPU; calls on one engine must be serialised by the caller except
  * where noted (the Python adapter holds a lock, like the reference's single
  * LMDB writer, fingerprint.py:7-8).
@@ -56,8 +58,14 @@ typedef struct aid_config {
     int32_t device;        /* HIP device ordinal; -1 = current device */
     int32_t min_match;     /* query: 0 = FPSPEC default 12 */
     int32_t max_results;   /* query: 0 = FPSPEC default 50 */
-    int32_t reserved[10];
+    int32_t flags;         /* AID_FLAG_* (0 = default) */
+    int32_t reserved[9];
 } aid_config;
+
+/* aid_config.flags: keep the whole power plane of an extraction for aid_result_power. Without it
+   K1 skips the stores of 64-bin blocks whose every power is <= peak_threshold (K2 never reads
+   them) and aid_result_power fails with AID_ERR_STATE. */
+#define AID_FLAG_KEEP_POWER 1
 
 /* one landmark record (FPSPEC 6): hash in the low word, anchor frame in the high word */
 typedef struct aid_hash {
@@ -105,7 +113,7 @@ int aid_result_device(aid_engine *e, const aid_hash **records, const int64_t **c
                       const int64_t **clip_base_host, int32_t *n_clips);
 
 /* Debug/parity views of the last extraction (host copies, synchronise):
-   power rows [F][1024] fp32 of clip `clip`; peak bitmask [F][16] uint64. */
+   power rows [F][1024] fp32 of clip `clip` (needs AID_FLAG_KEEP_POWER); peak bitmask [F][16] uint64. */
 int aid_result_power(aid_engine *e, int32_t clip, float *out, int64_t cap_floats);
 int aid_result_peakmask(aid_engine *e, int32_t clip, uint64_t *out, int64_t cap_words);
 

@@ -23,13 +23,24 @@ def _clip(tr, n, start=0, snr=None):
 
 
 def test_power_bit_exact(gpu_engine):
+    """With AID_FLAG_KEEP_POWER K1 stores every block: the power plane is the oracle's bit for bit.
+    Without it (the default, `gpu_engine`) cold blocks are not stored, power() fails loudly, and
+    the hashes are the same."""
+    from aidfp.engine import Engine
+
     clips = [_clip(1, 441000), _clip(2, 100000, start=12345, snr=20), _clip(3, 2048), _clip(4, 2049), _clip(5, 5000)]
-    gpu_engine.extract_host(clips)
-    for c, x in enumerate(clips):
-        P = gpu_engine.power(c, len(x))
-        R = O.stft_power(x, HOP)
-        assert P.shape == R.shape
-        assert np.array_equal(P.view(np.uint32), R.view(np.uint32)), f"clip {c}: power bits differ"
+    with Engine(SR, keep_power=True) as eng:
+        got_keep = eng.extract_host(clips)
+        for c, x in enumerate(clips):
+            P = eng.power(c, len(x))
+            R = O.stft_power(x, HOP)
+            assert P.shape == R.shape
+            assert np.array_equal(P.view(np.uint32), R.view(np.uint32)), f"clip {c}: power bits differ"
+    got = gpu_engine.extract_host(clips)
+    for c in range(len(clips)):
+        assert np.array_equal(got[c], got_keep[c])
+    with pytest.raises(Exception, match="KEEP_POWER"):
+        gpu_engine.power(0, len(clips[0]))
 
 
 def test_peaks_and_hashes_bit_exact(gpu_engine):
@@ -137,13 +148,15 @@ def test_back_to_back_calls_without_sync(gpu_engine):
     assert counts[1] == 0  # the 1000-sample clip has no frame
 
 
+@pytest.mark.parametrize("keep", [False, True])
 @pytest.mark.parametrize("hop", [128, 256, 1024, 2048])
-def test_every_hop_bit_exact(hop):
+def test_every_hop_bit_exact(hop, keep):
     """K1 is specialised per hop (hop/128 new PCM rows per frame): each specialisation is
-    bit-exact, power and hashes, including a long clip with several K3 chunks at hop 128."""
+    bit-exact, power (engine keeping the whole plane) and hashes (both store modes), including a
+    long clip with several K3 chunks at hop 128."""
     from aidfp.engine import Engine
 
-    with Engine(44100, hop=hop) as eng:
+    with Engine(44100, hop=hop, keep_power=keep) as eng:
         assert eng.hop == hop
         lens = [2048, 2048 + hop * 37 + 5, 44100 * 3, 44100 * 7 + 1]
         if hop == 128:
@@ -151,8 +164,9 @@ def test_every_hop_bit_exact(hop):
         clips = [_clip(70 + i, n, start=101 * i, snr=25 if i % 2 else None) for i, n in enumerate(lens)]
         got = eng.extract_host(clips)
         for c, x in enumerate(clips):
-            P = eng.power(c, len(x))
-            assert np.array_equal(P.view(np.uint32), O.stft_power(x, hop).view(np.uint32)), (hop, c)
+            if keep:
+                P = eng.power(c, len(x))
+                assert np.array_equal(P.view(np.uint32), O.stft_power(x, hop).view(np.uint32)), (hop, c)
             assert np.array_equal(got[c], O.fingerprint(x, hop)), (hop, c)
 
 
