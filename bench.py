@@ -166,6 +166,8 @@ def main() -> int:
         "algorithmic_bytes_per_launch": alg[dom],
         "traffic_source": pmc_src,
         "extraction_kernels_ms_per_step": round(sum(v["ms_per_launch"] for v in kern.values() if v["ms_per_launch"]), 4),
+        "note": "achieved = SURVEY 8(d) staged-dataflow bytes (PCM + the full power plane); K1 stores only hot "
+                "64-bin blocks and K2 reads only those, so the PMC traffic can be below the algorithmic bytes",
     }
 
     cpu = None
