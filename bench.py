@@ -94,6 +94,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--settle", type=float, default=0.1,
+                    help="seconds of untimed steps after the warmup steps (GPU clock ramp); 0 = none")
     args = ap.parse_args()
 
     import torch
@@ -124,6 +126,16 @@ def main() -> int:
     for _ in range(max(0, args.warmup)):
         eng.extract_device(pcm.data_ptr(), offs, stream)
     torch.cuda.synchronize()
+    # settle: keep stepping (untimed) until the GPU has been busy for SETTLE_S. An idle MI355X
+    # needs ~25 ms of load to reach its steady clocks: the first 20 steps after start-up (or after
+    # 0.5 s idle) ran K1 at 0.345 ms against 0.303 ms steady (probes/ramp_probe.py)
+    settle_steps = 0
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle:
+        for _ in range(10):
+            eng.extract_device(pcm.data_ptr(), offs, stream)
+        settle_steps += 10
+        torch.cuda.synchronize()
     hashes_per_step = int(eng.counts().sum())
 
     eng.profile_enable(True)
@@ -183,6 +195,7 @@ def main() -> int:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": settle_steps,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
