@@ -60,6 +60,15 @@
 #ifndef AID_K1_DPPC
 #define AID_K1_DPPC 2
 #endif
+// AID_K1_E1V=1: E1 read side as 8 ds_read_b128 instead of 16 ds_read_b64. Row k1 holds writer
+// lane n2 = 4 m1 + m2 at float2 slot 8 ((m1 >> 1) ^ (k1 & 7)) + 2 m2 + (m1 & 1), so the reader
+// (kq, mq) finds A[kq][4 (2j) + mq] and A[kq][4 (2j+1) + mq] side by side at 8 (j ^ (kq & 7)) + 2 mq.
+// Writes (4 x 16 contiguous lanes, bank = slot mod 16) and reads (4 x 16-lane groups of ds_read_b128,
+// float4 slot mod 16 = 4 ((j ^ kq) & 3) + mq) are both conflict-free. Same bytes, same LDS cycles,
+// half the read instructions.
+#ifndef AID_K1_E1V
+#define AID_K1_E1V 1
+#endif
 // AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
 // (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
 
@@ -94,7 +103,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                                                 uint32_t *__restrict__ hot, float thr, int keep) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
-    __shared__ float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
+    __shared__ __attribute__((aligned(16))) float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
     // tables as float4 pairs [h][lane], one ds_read_b128 per pair (hipcc would otherwise merge the
     // stride-512-B float2 reads into ds_read2st64_b64, which costs the LDS twice the cycles):
     //   s_win4[h] = window of rows 2h, 2h+1 ; s_ta4[h] = T1K[lane*k1], k1 = 2h, 2h+1
@@ -227,6 +236,19 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
                 if (AID_K1_DIAG != 6) {
+#if AID_K1_E1V
+#pragma unroll
+                    for (int k1 = 0; k1 < 16; ++k1)
+                        buf[k1 * 64 + 8 * ((kq >> 1) ^ (k1 & 7)) + 2 * mq + (kq & 1)] = v[k1];
+                    wave_lds_sync();
+                    const float4 *buf4 = reinterpret_cast<const float4 *>(buf);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const float4 q = buf4[kq * 32 + 4 * (j ^ (kq & 7)) + mq];
+                        v[2 * j] = make_float2(q.x, q.y);
+                        v[2 * j + 1] = make_float2(q.z, q.w);
+                    }
+#else
 #pragma unroll
                     for (int k1 = 0; k1 < 16; ++k1)
                         buf[AID_K1_COMPACT ? k1 * 64 + (lane ^ (4 * (k1 & 7))) : k1 * 68 + lane] = v[k1];
@@ -236,6 +258,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         v[m1] = buf[AID_K1_DIAG == 4    ? m1 * 68 + lane
                                     : AID_K1_COMPACT ? kq * 64 + 4 * ((m1 & 8) | ((m1 ^ kq) & 7)) + mq
                                                      : kq * 68 + 4 * m1 + mq];
+#endif
                     wave_lds_sync();
                 }
                 // stage B
