@@ -123,6 +123,7 @@ SIGNATURES = [
     ("aid_dedup_pairs", ctypes.c_int, [P, P, P, P, P, I32, P]),
     ("aid_profile_enable", ctypes.c_int, [P, I32]),
     ("aid_profile_read", ctypes.c_int, [P, P, P, I32]),
+    ("aid_profile_select", ctypes.c_int, [P, ctypes.c_uint32]),
 ]
 
 _lib = None

@@ -331,6 +331,11 @@ class Engine:
     def profile_enable(self, on: bool = True) -> None:
         check(self._lib.aid_profile_enable(self._h, 1 if on else 0))
 
+    def profile_select(self, kernels) -> None:
+        """Restrict profiling events to these kernel ids (AID_K_*); None = all."""
+        mask = 0xFFFFFFFF if kernels is None else sum(1 << int(k) for k in kernels)
+        check(self._lib.aid_profile_select(self._h, ctypes.c_uint32(mask)))
+
     def profile_read(self, reset: bool = False) -> dict:
         ms = np.zeros(L.AID_K_COUNT, dtype=np.float64)
         n = np.zeros(L.AID_K_COUNT, dtype=np.int64)

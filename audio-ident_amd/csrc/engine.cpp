@@ -197,6 +197,7 @@ struct aid_engine {
     bool have_result = false;
 
     bool profiling = false;
+    uint32_t prof_mask = 0xFFFFFFFFu;  // bit k: kernel id k gets events (aid_profile_select)
     std::vector<ProfEvent> pending;
     std::vector<hipEvent_t> pool;
     double prof_ms[AID_K_COUNT] = {};
@@ -224,7 +225,7 @@ struct ProfScope {
     bool attached;
     hipEvent_t a = nullptr, b = nullptr;
     ProfScope(aid_engine *e_, int k_, hipStream_t s_, bool attached_ = false) : e(e_), k(k_), s(s_), attached(attached_) {
-        if (!e->profiling || !(a = take_event(e))) return;
+        if (!e->profiling || !((e->prof_mask >> k) & 1u) || !(a = take_event(e))) return;
         if (!attached) {
             (void)hipEventRecord(a, s);
             return;
@@ -922,6 +923,13 @@ int aid_dedup_pairs(aid_engine *e, const uint32_t *a, const int64_t *a_off, cons
 int aid_profile_enable(aid_engine *e, int32_t on) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     e->profiling = on != 0;
+    return AID_OK;
+}
+
+int aid_profile_select(aid_engine *e, uint32_t kernel_mask) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->prof_mask = kernel_mask;
     return AID_OK;
 }
 

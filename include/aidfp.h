@@ -244,6 +244,10 @@ int aid_downmix(aid_engine *e, const float *stereo, int64_t n_frames, float *mon
 
 /* Per-kernel timing with HIP events recorded on the launch stream. */
 int aid_profile_enable(aid_engine *e, int32_t on);
+/* Which kernels get events while profiling is on: bit k = kernel id k (AID_K_*); default all.
+   Each timed launch carries two dispatch-attached events (~5 us of end-of-kernel work per launch on
+   MI355X), so a bench can time only the kernels it reports. */
+int aid_profile_select(aid_engine *e, uint32_t kernel_mask);
 /* ms[AID_K_COUNT] summed device time, launches[AID_K_COUNT]; synchronises; reset != 0 clears. */
 int aid_profile_read(aid_engine *e, double *ms, int64_t *launches, int32_t reset);
 

@@ -20,8 +20,10 @@ s = torch.cuda.current_stream().cuda_stream
 for _ in range(3):
     eng.extract_device(pcm.data_ptr(), offs, s)
 torch.cuda.synchronize()
-for rep in range(3):
-    for prof in (False, True):
+REPS = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+for rep in range(REPS):
+    for prof, sel in ((False, None), (True, None), (True, (0, 1)), (True, (0,))):
+        eng.profile_select(sel)
         eng.profile_enable(prof)
         eng.profile_read(reset=True)
         torch.cuda.synchronize()
@@ -32,4 +34,4 @@ for rep in range(3):
         dt = (time.perf_counter() - t0) / K
         p = eng.profile_read(reset=True)
         ks = {k: round(ms / c, 4) for k, (ms, c) in p.items() if c}
-        print(f"prof={prof} ms/step {dt * 1e3:.4f} audio-s/s {CLIPS * CLIP_S / dt:.0f} {ks}", flush=True)
+        print(f"prof={prof} sel={sel} ms/step {dt * 1e3:.4f} audio-s/s {CLIPS * CLIP_S / dt:.0f} {ks}", flush=True)
