@@ -201,3 +201,28 @@ def test_nonfinite_huge_and_tied_inputs(gpu_engine):
         pk = peaks_from_mask(gpu_engine.peakmask(i, len(x)))
         assert np.array_equal(pk, ref_pk.reshape(-1, 2)), f"clip {i}: peaks differ"
         assert np.array_equal(got[i], O.fingerprint(x, HOP)), f"clip {i}: hashes differ"
+
+
+def test_profile_select_masks_kernels(gpu_engine):
+    """aid_profile_select: only the selected kernels get events (bench.py times K1 alone inside its
+    timed region); the hashes are unchanged and `None` restores every kernel."""
+    clips = [_clip(70 + i, 44100 * 2 + 512 * i) for i in range(3)]
+    ref = [O.fingerprint(x, HOP) for x in clips]
+    try:
+        gpu_engine.profile_select([0])
+        gpu_engine.profile_enable(True)
+        gpu_engine.profile_read(reset=True)
+        got = gpu_engine.extract_host(clips)
+        prof = gpu_engine.profile_read(reset=True)
+        assert prof["stft_power"][1] == 1 and prof["stft_power"][0] > 0
+        assert all(cnt == 0 for k, (_, cnt) in prof.items() if k != "stft_power")
+        for g, r in zip(got, ref):
+            assert np.array_equal(g, r)
+        gpu_engine.profile_select(None)
+        gpu_engine.extract_host(clips)
+        prof = gpu_engine.profile_read(reset=True)
+        assert prof["stft_power"][1] == 1 and prof["peak_pick"][1] == 1
+    finally:
+        gpu_engine.profile_enable(False)
+        gpu_engine.profile_select(None)
+        gpu_engine.profile_read(reset=True)
