@@ -27,6 +27,33 @@ namespace aid {
 
 constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
 
+#ifndef AID_K3_WSCAN
+#define AID_K3_WSCAN 1  // 1: wave scans (shuffles) + one LDS exchange of wave totals: 2 barriers per scan, not 20
+#endif
+
+#if AID_K3_WSCAN
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK3]*/, int64_t *total) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int64_t x = v;  // inclusive scan over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) tmp[w] = x;
+    __syncthreads();
+    int64_t base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kK3 / 64; ++i) {
+        const int64_t t = tmp[i];
+        base += i < w ? t : 0;
+        tot += t;
+    }
+    if (total) *total = tot;
+    __syncthreads();  // every wave has read tmp before the next scan writes it
+    return base + x - v;
+}
+#else
 __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK3]*/, int64_t *total) {
     const int tid = threadIdx.x;
     tmp[tid] = v;
@@ -43,6 +70,7 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK
     __syncthreads();
     return incl - v;
 }
+#endif
 
 // bit l of x (l < 16) -> bit 4l
 __device__ __forceinline__ uint64_t spread4(uint64_t x) {
