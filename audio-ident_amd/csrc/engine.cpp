@@ -339,6 +339,14 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     }
     Tables *h = new Tables();
     build_tables(*h);
+    // K1 (AID_K1_T2HALF) derives the real split's mirror twiddle T2K[1024-k] as (-re, im) of T2K[k]
+    for (int k = 1; k < 512; ++k)
+        if (!(h->t2k[1024 - k].x == -h->t2k[k].x && h->t2k[1024 - k].y == h->t2k[k].y)) {
+            delete h;
+            (void)hipStreamDestroy(e->own_stream);
+            delete e;
+            return fail(AID_ERR_DEVICE, "twiddle table lacks the mirror symmetry K1 relies on");
+        }
     std::vector<int16_t> sin_tab(4096);
     for (int k = 0; k < 4096; ++k) sin_tab[k] = (int16_t)nearbyint(32767.0 * sin(2.0 * M_PI * (double)k / 4096.0));
     he = hipMalloc(&e->d_tab, sizeof(Tables));

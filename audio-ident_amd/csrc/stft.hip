@@ -66,6 +66,12 @@
 // Writes (4 x 16 contiguous lanes, bank = slot mod 16) and reads (4 x 16-lane groups of ds_read_b128,
 // float4 slot mod 16 = 4 ((j ^ kq) & 3) + mq) are both conflict-free. Same bytes, same LDS cycles,
 // half the read instructions.
+// AID_K1_T2HALF=1: the real split's mirror twiddle T2K[1024-k] is taken as (-re, im) of T2K[k] (the
+// host tables satisfy it exactly for every k, checked in aid_engine_create), so the split table is
+// float2 [512] read with ds_read_b64 instead of float4 pairs with ds_read_b128 (half the LDS bytes)
+#ifndef AID_K1_T2HALF
+#define AID_K1_T2HALF 1
+#endif
 #ifndef AID_K1_E1V
 #define AID_K1_E1V 1
 #endif
@@ -108,7 +114,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     // stride-512-B float2 reads into ds_read2st64_b64, which costs the LDS twice the cycles):
     //   s_win4[h] = window of rows 2h, 2h+1 ; s_ta4[h] = T1K[lane*k1], k1 = 2h, 2h+1
     //   s_tb4[h] = T64[(lane&3)*j1], j1 = 2h, 2h+1 ; s_t2p[i] = (T2K[k], T2K[1024-k]), k = lane + 64i
-    __shared__ float4 s_win4[512], s_ta4[512], s_t2p[512];
+    __shared__ float4 s_win4[512], s_ta4[512];
+#if AID_K1_T2HALF
+    __shared__ float2 s_t2[512];  // T2K[k], k < 512
+#else
+    __shared__ float4 s_t2p[512];
+#endif
     __shared__ float4 s_tb4[32];  // [h][lane & 3]: T64[m2*j1] depends on the lane only through m2
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar strip/segment math
@@ -151,8 +162,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
             s_tb4[4 * h + l] = make_float4(tb0.x, tb0.y, tb1.x, tb1.y);
         }
         const int k = l + 64 * h;
+#if AID_K1_T2HALF
+        s_t2[i] = tab->t2k[k];
+#else
         const float2 c0 = tab->t2k[k], c1 = tab->t2k[(1024 - k) & 1023];  // k = 0: mirror unused
         s_t2p[i] = make_float4(c0.x, c0.y, c1.x, c1.y);
+#endif
     }
     const float2 t512 = tab->t2k[512];
     float2 t16[10];
@@ -397,7 +412,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
                     const float er = a.x + b.x, ei = a.y - b.y;
                     const float orr = a.y + b.y, oi = b.x - a.x;
+#if AID_K1_T2HALF
+                    const float2 t2h = s_t2[64 * i + lane];
+                    const float4 t2 = make_float4(t2h.x, t2h.y, -t2h.x, t2h.y);  // T2K[1024-k] = (-re, im)
+#else
                     const float4 t2 = s_t2p[64 * i + lane];
+#endif
                     {
                         const float2 tw = cmul(make_float2(orr, oi), make_float2(t2.x, t2.y));
                         const float xr = er + tw.x, xi = ei + tw.y;
