@@ -43,6 +43,9 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_ROT
 #define AID_K2_ROT 1  // rotate the wave -> bin-quarter map by blockIdx (SIMD load balance)
 #endif
+#ifndef AID_K2_FULL128
+#define AID_K2_FULL128 0  // 1: whole-block ds_read_b128 for the far blocks j-4 / j+4 instead of ds_read_b96: measured neutral (K2 0.1910 vs 0.1907 ms)
+#endif
 #ifndef AID_K2_DIAG
 #define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
 #endif
@@ -242,6 +245,10 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             const int4 *rb4 = reinterpret_cast<const int4 *>(rows[buf][s % kRowsPerStep]);
             const int *bm = bms[buf][s % kRowsPerStep];
             const int4 lf = rb4[tid], me = rb4[tid + 4], rt = rb4[tid + 8];  // blocks j-4, j, j+4
+#if AID_K2_FULL128
+            // keep lf.x / rt.w live so hipcc issues ds_read_b128, not ds_read_b96 (lf uses bins 1..3, rt 0..2)
+            asm volatile("" ::"v"(lf.x), "v"(rt.w));
+#endif
             const int M3L = max(max(bm[tid + 1], bm[tid + 2]), bm[tid + 3]);  // blocks j-3..j-1
             const int M3R = max(max(bm[tid + 5], bm[tid + 6]), bm[tid + 7]);  // blocks j+1..j+3
             const int lsuf2 = max(lf.z, lf.w), lsuf1 = max(lf.y, lsuf2);      // block j-4: bins 1..3, 2..3
