@@ -44,7 +44,7 @@ constexpr int kRowsPerStep = 4;
 #define AID_K2_ROT 1  // rotate the wave -> bin-quarter map by blockIdx (SIMD load balance)
 #endif
 #ifndef AID_K2_FULL128
-#define AID_K2_FULL128 0  // 1: whole-block ds_read_b128 for the far blocks j-4 / j+4 instead of ds_read_b96: measured neutral (K2 0.1910 vs 0.1907 ms)
+#define AID_K2_FULL128 1  // whole-block ds_read_b128 for the far blocks j-4 / j+4 instead of ds_read_b96: K2 LDS bank conflicts 8.2 M -> 0 cycles, LDS-array cycles 31.0 M -> 20.2 M; time neutral (0.1910 vs 0.1907 ms)
 #endif
 #ifndef AID_K2_DIAG
 #define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
