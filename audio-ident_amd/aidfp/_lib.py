@@ -97,7 +97,9 @@ SIGNATURES = [
     ("aid_index_reset", ctypes.c_int, [P]),
     ("aid_index_add_extracted", ctypes.c_int, [P, P]),
     ("aid_index_add_postings", ctypes.c_int, [P, P, P, P, I64, I32]),
+    ("aid_index_add_track", ctypes.c_int, [P, ctypes.c_uint32]),
     ("aid_index_remove", ctypes.c_int, [P, ctypes.c_uint32]),
+    ("aid_index_compact", ctypes.c_int, [P, P]),
     ("aid_index_finalize", ctypes.c_int, [P]),
     ("aid_index_stats", ctypes.c_int, [P, P, P, P]),
     ("aid_index_export", ctypes.c_int, [P, P, P, P, I64, I64, I32]),

@@ -176,6 +176,9 @@ class Engine:
         h = np.ascontiguousarray((rec & np.uint64(0xFFFFFFFF)).astype(np.uint32))
         t = np.ascontiguousarray((rec >> np.uint64(32)).astype(np.uint32))
         tr = np.full(len(rec), track, dtype=np.uint32)
+        if len(rec) == 0:  # no hashes (short/quiet clip): the id still gets a slot, so it can be removed
+            check(self._lib.aid_index_add_track(self._h, int(track)))
+            return
         check(self._lib.aid_index_add_postings(self._h, _p(h), _p(tr), _p(t), len(rec), AID_PCM_HOST))
 
     def index_add_postings(self, hash_ptr: int, track_ptr: int, t_ptr: int, n: int, device: bool = True) -> None:
@@ -184,6 +187,12 @@ class Engine:
 
     def index_remove(self, track: int) -> None:
         check(self._lib.aid_index_remove(self._h, int(track)))
+
+    def index_compact(self) -> int:
+        """Drop the stored postings of removed tracks; returns how many were dropped."""
+        n = ctypes.c_int64()
+        check(self._lib.aid_index_compact(self._h, ctypes.byref(n)))
+        return int(n.value)
 
     def index_finalize(self) -> None:
         check(self._lib.aid_index_finalize(self._h))

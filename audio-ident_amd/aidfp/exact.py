@@ -211,19 +211,21 @@ async def run_exact_lane_batch(clips: Sequence[bytes], max_results: int = 10, *,
                                lookup: LookupFn | None = None) -> list[list[ExactMatch]]:
     """run_exact_lane for a batch of 16 kHz f32le clips in one engine call (aid_exact_lane):
     sub-window fan-out, K1-K5 and the consensus/threshold/ranking kernel on the GPU; only the
-    metadata lookup runs here. An engine failure gives [] for every clip (the reference logs a
-    failed olaf query and carries on, exact.py:163-171)."""
+    metadata lookup runs here. An engine failure, including an engine that cannot start
+    (OlafError), gives [] for every clip: the reference logs a failed olaf query and carries on
+    (exact.py:163-171 sub-windows, :186-190 full clip)."""
     import asyncio
 
     from .fingerprint import get_service
 
-    svc = service or get_service()
     if not clips:
         return []
     try:
+        svc = service or get_service()
         ranked = await asyncio.get_running_loop().run_in_executor(None, svc.exact_batch, list(clips), max_results)
     except OlafError:
-        raise
+        logger.exception("exact lane: fingerprint engine unavailable")
+        ranked = [[] for _ in clips]
     except Exception:
         logger.exception("batched exact lane failed")
         ranked = [[] for _ in clips]

@@ -11,7 +11,7 @@ runs in-process on the GPU engine (libaidfp.so) instead of spawning the external
   olaf_query(pcm) -> list[OlafMatch] (:158)   extract + K5 match on GPU, count desc
   olaf_delete_track(uuid) -> bool (:222)      tombstone + persist
   _parse_olaf_output/_line/_parts (:273-350)  same parsing (used by the CLI shim)
-  OLAF_DB dir (:71-84)                        same dir: index.aidfp + tracks.json
+  OLAF_DB dir (:71-84)                        same dir: snapshot + journal (aidfp.store)
 
 Error contract (reference :102-155, :173-219, :234-270):
   * empty PCM -> False / [] without touching the engine;
@@ -28,7 +28,6 @@ the event loop is never blocked.
 from __future__ import annotations
 
 import asyncio
-import json
 import logging
 import os
 import threading
@@ -97,49 +96,96 @@ def db_path() -> Path:
 
 
 class FingerprintService:
-    """One GPU engine + the persisted index of the OLAF_DB directory."""
+    """One GPU engine + the persisted index of the OLAF_DB directory (aidfp.store: snapshot +
+    write-ahead journal, so a store or delete writes O(track) bytes, not the whole index)."""
 
-    def __init__(self, db_dir: Path | None = None, device: int = -1):
+    def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20):
         self.db_dir = Path(db_dir) if db_dir is not None else db_path()
         self.device = device
         self._lock = threading.Lock()
         self._engine = None
+        self._store = None
         self._ids: dict[str, int] = {}  # uuid string -> engine track id
         self._names: dict[int, str] = {}
         self._next = 0
         self.persist = True
+        self.checkpoint_min_bytes = checkpoint_min_bytes
 
     # -- engine and persistence --
     def _eng(self):
+        """The engine, created and loaded from the OLAF_DB directory on first use. The service
+        keeps it only once the saved index has been loaded completely: a failed load destroys
+        the engine and raises OlafError, so nothing is ever written over a catalog that was not
+        read (the next call retries the load)."""
         if self._engine is None:
             from ._lib import EngineError, EngineUnavailable
             from .engine import Engine
+            from .store import OP_STORE, IndexStore, StoreCorrupt
 
             try:
-                self._engine = Engine(SAMPLE_RATE, device=self.device)
+                eng = Engine(SAMPLE_RATE, device=self.device)
             except (EngineUnavailable, EngineError, OSError) as exc:
                 raise OlafError(f"fingerprint engine binary not found or unusable (libaidfp.so): {exc}") from exc
-            self._load()
+            store = IndexStore(self.db_dir, self.checkpoint_min_bytes)
+            ids: dict[str, int] = {}
+            names: dict[int, str] = {}
+            try:
+                if self.persist:
+                    ids, nxt, entries = store.load(eng)
+                    names = {v: k for k, v in ids.items()}
+                    for op, track, name, recs in entries:  # replay the journal in order
+                        if op == OP_STORE:
+                            self._apply_store(eng, ids, names, track, name, recs)
+                        else:
+                            self._apply_delete(eng, ids, names, track, name)
+                else:
+                    nxt = 0
+                    store.loaded = True
+            except (EngineError, StoreCorrupt, OSError) as exc:
+                eng.close()
+                raise OlafError(f"cannot load the fingerprint index in {self.db_dir}: {exc}") from exc
+            except BaseException:
+                eng.close()
+                raise
+            self._engine, self._store = eng, store
+            self._ids, self._names, self._next = ids, names, nxt
         return self._engine
 
-    def _load(self) -> None:
-        idx, meta = self.db_dir / "index.aidfp", self.db_dir / "tracks.json"
-        if idx.exists() and meta.exists():
-            self._engine.index_load(str(idx))
-            d = json.loads(meta.read_text())
-            self._ids = {k: int(v) for k, v in d["ids"].items()}
-            self._names = {v: k for k, v in self._ids.items()}
-            self._next = int(d["next"])
+    @staticmethod
+    def _apply_store(eng, ids, names, track: int, name: str, recs) -> None:
+        """A store of `name` as `track` (the journal's replay and the live path do the same)."""
+        eng.index_add_records(track, recs)
+        old = ids.get(name)
+        if old is not None and old != track:  # re-store replaces the previous fingerprints
+            FingerprintService._remove_quiet(eng, old)
+            names.pop(old, None)
+        ids[name] = track
+        names[track] = name
 
-    def _save(self) -> None:
-        if not self.persist:
-            return
-        self.db_dir.mkdir(parents=True, exist_ok=True)
-        tmp = self.db_dir / "index.aidfp.tmp"
-        self._engine.index_save(str(tmp))
-        os.replace(tmp, self.db_dir / "index.aidfp")
-        (self.db_dir / "tracks.json.tmp").write_text(json.dumps({"ids": self._ids, "next": self._next}))
-        os.replace(self.db_dir / "tracks.json.tmp", self.db_dir / "tracks.json")
+    @staticmethod
+    def _remove_quiet(eng, track: int) -> None:
+        """Replay: an id without an engine slot (a zero-hash track of an older index) has nothing
+        to remove."""
+        from ._lib import EngineError
+
+        try:
+            eng.index_remove(track)
+        except EngineError as exc:
+            logger.warning("aidfp journal replay: remove of track %d: %s", track, exc)
+
+    @staticmethod
+    def _apply_delete(eng, ids, names, track: int, name: str) -> None:
+        FingerprintService._remove_quiet(eng, track)
+        if ids.get(name) == track:
+            del ids[name]
+        names.pop(track, None)
+
+    def _maybe_checkpoint(self) -> None:
+        if self.persist and self._store.should_checkpoint():
+            try:
+                self._store.checkpoint(self._engine, dict(self._ids), self._next)
+            except OSError:  # the journal still holds every operation: nothing is lost
+                logger.exception("aidfp index checkpoint failed (journal kept)")
 
     @staticmethod
     def _pcm(buf: bytes) -> np.ndarray:
@@ -153,20 +199,35 @@ class FingerprintService:
             eng = self._eng()
             try:
                 recs = eng.extract_host([self._pcm(pcm)])[0]
-                old = self._ids.get(name)
-                if old is not None:  # re-store replaces the previous fingerprints
-                    eng.index_remove(old)
-                    self._names.pop(old, None)
                 tid = self._next
-                self._next += 1
+                # the new postings first, the journal entry, then the old ones go: a failed
+                # append leaves the previous fingerprints of `name` live
                 eng.index_add_records(tid, recs)
-                self._ids[name] = tid
-                self._names[tid] = name
-                self._save()
-                return True
+                self._next += 1
             except EngineError as exc:
                 logger.error("aidfp store failed for %s: %s", name, exc)
                 return False
+            if self.persist:
+                try:
+                    self._store.append_store(tid, name, recs)
+                except OSError as exc:
+                    logger.error("aidfp store of %s not persisted: %s", name, exc)
+                    eng.index_remove(tid)
+                    return False
+            try:
+                self._apply_store_maps(eng, name, tid)
+            except EngineError as exc:
+                logger.error("aidfp store of %s: removing the previous fingerprints failed: %s", name, exc)
+            self._maybe_checkpoint()
+            return True
+
+    def _apply_store_maps(self, eng, name: str, tid: int) -> None:
+        old = self._ids.get(name)
+        self._ids[name] = tid
+        self._names[tid] = name
+        if old is not None and old != tid:
+            self._names.pop(old, None)
+            eng.index_remove(old)
 
     def query(self, pcm: bytes) -> list[OlafMatch]:
         from ._lib import EngineError
@@ -222,8 +283,21 @@ class FingerprintService:
                 return False
             del self._ids[name]
             self._names.pop(tid, None)
-            self._save()
+            if self.persist:
+                try:
+                    self._store.append_delete(tid, name)
+                except OSError as exc:  # removed now, but it comes back after a restart
+                    logger.error("aidfp del of %s not persisted: %s", name, exc)
+                    return False
+            self._maybe_checkpoint()
             return True
+
+    def checkpoint(self) -> None:
+        """Fold the journal into a new snapshot now (compacting removed tracks' postings)."""
+        with self._lock:
+            self._eng()
+            if self.persist:
+                self._store.checkpoint(self._engine, dict(self._ids), self._next)
 
     def close(self) -> None:
         with self._lock:

@@ -46,6 +46,9 @@ void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, c
 void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                           const uint8_t *tomb, uint32_t n_tracks, uint32_t *cursor, uint64_t *post, hipStream_t s);
 void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
+void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
+                    uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
+                    uint32_t *ot, hipStream_t s);
 void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
                                 const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
@@ -1080,6 +1083,18 @@ int aid_index_add_postings(aid_engine *e, const uint32_t *hash, const uint32_t *
     return AID_OK;
 }
 
+int aid_index_add_track(aid_engine *e, uint32_t track) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    if (track == 0xFFFFFFFFu) return fail(AID_ERR_INVALID, "aid_index_add_track: bad track id");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    if (int rc = ensure_tracks(e, track + 1, s)) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    return AID_OK;
+}
+
 int aid_index_remove(aid_engine *e, uint32_t track) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);
@@ -1088,6 +1103,48 @@ int aid_index_remove(aid_engine *e, uint32_t track) {
     e->h_tomb[track] = 1;
     ++e->tomb_since_build;  // the CSR still holds its postings until the next finalize
     HIP_TRY(hipMemcpy(e->tomb.p + track, &e->h_tomb[track], 1, hipMemcpyHostToDevice));
+    return AID_OK;
+}
+
+int aid_index_compact(aid_engine *e, int64_t *n_removed) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (n_removed) *n_removed = 0;
+    bool any = false;
+    for (uint8_t t : e->h_tomb) any = any || t;
+    if (!any || e->n_post == 0) return AID_OK;
+    if (e->n_post > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index holds more than 2^32 postings");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->own_stream;
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    const int64_t nb = (e->n_post + 1023) / 1024;
+    DevBuf<uint32_t> cnt, off, tmp, nh, ntr, nt;
+    struct Release {  // every scratch buffer goes on every return path
+        DevBuf<uint32_t> *b[6];
+        ~Release() {
+            for (auto *x : b) x->release();
+        }
+    } release_all{{&cnt, &off, &tmp, &nh, &ntr, &nt}};
+    HIP_TRY(cnt.reserve((size_t)nb));
+    HIP_TRY(off.reserve((size_t)nb));
+    HIP_TRY(tmp.reserve(4 * ((size_t)nb / 1024 + 2) + 4096));
+    HIP_TRY(nh.reserve((size_t)e->n_post));
+    HIP_TRY(ntr.reserve((size_t)e->n_post));
+    HIP_TRY(nt.reserve((size_t)e->n_post));
+    launch_compact(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks, cnt.p, off.p, tmp.p, nh.p,
+                   ntr.p, nt.p, s);
+    HIP_TRY(hipGetLastError());
+    uint32_t last_off = 0, last_cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&last_off, off.p + (nb - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&last_cnt, cnt.p + (nb - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const int64_t live = (int64_t)last_off + last_cnt;
+    if (n_removed) *n_removed = e->n_post - live;
+    std::swap(e->p_hash, nh);
+    std::swap(e->p_track, ntr);
+    std::swap(e->p_t, nt);  // the old planes are released with the scratch buffers
+    e->n_post = live;  // tombstones stay: removed ids are never reused, and the CSR skips nothing new
+    e->index_dirty = true;
     return AID_OK;
 }
 
@@ -1286,38 +1343,68 @@ int aid_index_load(aid_engine *e, const char *path) {
     if (!e || !path) return fail(AID_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
-    FILE *f = std::fopen(path, "rb");
+    // Everything is validated and read into scratch buffers first; the engine's index changes only
+    // once the whole file has been read (a failed load leaves the previous index untouched).
+    struct File {
+        FILE *f;
+        ~File() {
+            if (f) std::fclose(f);
+        }
+    } file{std::fopen(path, "rb")};
+    FILE *f = file.f;
     if (!f) return fail(AID_ERR_INVALID, std::string("cannot open ") + path);
     char magic[8];
     int64_t hdr[6];
-    if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kIdxMagic, 8) != 0 || std::fread(hdr, sizeof(hdr), 1, f) != 1) {
-        std::fclose(f);
+    if (std::fread(magic, 1, 8, f) != 8 || std::memcmp(magic, kIdxMagic, 8) != 0 || std::fread(hdr, sizeof(hdr), 1, f) != 1)
         return fail(AID_ERR_INVALID, "not an aidfp index file");
-    }
-    if (hdr[1] != e->cfg.sample_rate || hdr[2] != e->cfg.hop) {
-        std::fclose(f);
+    if (hdr[0] != AID_ABI_VERSION) return fail(AID_ERR_INVALID, "index file written by another ABI version");
+    if (hdr[1] != e->cfg.sample_rate || hdr[2] != e->cfg.hop)
         return fail(AID_ERR_INVALID, "index sample_rate/hop differ from the engine's");
-    }
     const int64_t n = hdr[3];
+    if (n < 0 || n > 0xFFFFFFFFll || hdr[4] < 0 || hdr[4] > 0xFFFFFFFFll || hdr[5] != 0)
+        return fail(AID_ERR_INVALID, "corrupt index header");
     const uint32_t nt = (uint32_t)hdr[4];
-    hipStream_t s = e->own_stream;
-    e->n_post = 0;
-    if (int rc = reserve_postings(e, n, s)) { std::fclose(f); return rc; }
+    if (std::fseek(f, 0, SEEK_END) != 0) return fail(AID_ERR_INVALID, "cannot size index file");
+    const long long fsize = (long long)ftello(f);
+    const long long want = 8 + (long long)sizeof(hdr) + 12ll * n + (long long)nt;
+    if (fsize != want) return fail(AID_ERR_INVALID, fsize < want ? "truncated index file" : "index file has trailing bytes");
+    if (std::fseek(f, 8 + (long)sizeof(hdr), SEEK_SET) != 0) return fail(AID_ERR_INVALID, "cannot read index file");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    DevBuf<uint32_t> cols[3];
+    struct Release {
+        DevBuf<uint32_t> *c;
+        ~Release() {
+            for (int i = 0; i < 3; ++i) c[i].release();
+        }
+    } release_cols{cols};
     std::vector<uint32_t> buf((size_t)std::min<int64_t>(std::max<int64_t>(n, 1), 1 << 24));
-    DevBuf<uint32_t> *cols[3] = {&e->p_hash, &e->p_track, &e->p_t};
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 3; ++c) {
+        HIP_TRY(cols[c].reserve((size_t)std::max<int64_t>(n, 1)));
         for (int64_t o = 0; o < n; o += (int64_t)buf.size()) {
             const int64_t m = std::min<int64_t>((int64_t)buf.size(), n - o);
-            if (std::fread(buf.data(), sizeof(uint32_t), m, f) != (size_t)m) { std::fclose(f); return fail(AID_ERR_INVALID, "truncated index file"); }
-            HIP_TRY(hipMemcpy(cols[c]->p + o, buf.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice));
+            if (std::fread(buf.data(), sizeof(uint32_t), m, f) != (size_t)m) return fail(AID_ERR_INVALID, "truncated index file");
+            HIP_TRY(hipMemcpy(cols[c].p + o, buf.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice));
         }
-    e->n_tracks = 0;
-    e->h_tomb.clear();
-    if (int rc = ensure_tracks(e, nt, s)) { std::fclose(f); return rc; }
-    if (nt && std::fread(e->h_tomb.data(), 1, nt, f) != nt) { std::fclose(f); return fail(AID_ERR_INVALID, "truncated index file"); }
-    std::fclose(f);
-    if (nt) HIP_TRY(hipMemcpy(e->tomb.p, e->h_tomb.data(), nt, hipMemcpyHostToDevice));
+    }
+    std::vector<uint8_t> tomb(nt);
+    if (nt && std::fread(tomb.data(), 1, nt, f) != nt) return fail(AID_ERR_INVALID, "truncated index file");
+    DevBuf<uint8_t> dtomb;
+    struct ReleaseTomb {
+        DevBuf<uint8_t> *b;
+        ~ReleaseTomb() { b->release(); }
+    } release_tomb{&dtomb};
+    HIP_TRY(dtomb.reserve(std::max<size_t>(nt, 1024)));
+    if (nt) HIP_TRY(hipMemcpy(dtomb.p, tomb.data(), nt, hipMemcpyHostToDevice));
+    // commit: swap the new planes in (the old ones are released with the scratch)
+    std::swap(e->tomb, dtomb);
+    std::swap(e->p_hash, cols[0]);
+    std::swap(e->p_track, cols[1]);
+    std::swap(e->p_t, cols[2]);
+    e->h_tomb = std::move(tomb);
+    e->n_tracks = nt;
     e->n_post = n;
+    e->tomb_since_build = 0;
     e->index_dirty = true;
     e->index_built = false;
     return AID_OK;

@@ -94,6 +94,66 @@ __global__ __launch_bounds__(1024) void k_scan_add(uint32_t *__restrict__ out, c
     if (i < n) out[i] += boff[blockIdx.x];
 }
 
+void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
+
+// ---- posting compaction (aid_index_compact): drop the postings of removed tracks, order kept ----
+// The store's LMDB delete (`olaf_c del`, fingerprint.py:239-246) frees the track's entries; here a
+// removal only tombstones the track, and compaction reclaims its postings. 1024 postings per block.
+__device__ __forceinline__ bool posting_live(const uint32_t *ptrack, int64_t i, int64_t n, const uint8_t *tomb,
+                                             uint32_t n_tracks) {
+    if (i >= n) return false;
+    const uint32_t tr = ptrack[i];
+    return !(tr < n_tracks && tomb[tr]);
+}
+
+__global__ __launch_bounds__(1024) void k_compact_count(const uint32_t *__restrict__ ptrack, int64_t n,
+                                                        const uint8_t *__restrict__ tomb, uint32_t n_tracks,
+                                                        uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t s_w[16];
+    const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    const uint64_t b = __ballot(posting_live(ptrack, i, n, tomb, n_tracks));
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(b);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < 16; ++w) t += s_w[w];
+        cnt[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_compact_scatter(const uint32_t *__restrict__ ph, const uint32_t *__restrict__ ptrack,
+                                                          const uint32_t *__restrict__ pt, int64_t n,
+                                                          const uint8_t *__restrict__ tomb, uint32_t n_tracks,
+                                                          const uint32_t *__restrict__ off, uint32_t *__restrict__ oh,
+                                                          uint32_t *__restrict__ otrack, uint32_t *__restrict__ ot) {
+    __shared__ uint32_t s_w[16];
+    const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    const bool live = posting_live(ptrack, i, n, tomb, n_tracks);
+    const uint64_t b = __ballot(live);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t base = off[blockIdx.x];
+    for (int q = 0; q < w; ++q) base += s_w[q];
+    if (live) {
+        const uint32_t o = base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+        oh[o] = ph[i];
+        otrack[o] = ptrack[i];
+        ot[o] = pt[i];
+    }
+}
+
+void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
+                    uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
+                    uint32_t *ot, hipStream_t s) {
+    const int64_t nb = (n + 1023) / 1024;
+    if (nb <= 0) return;
+    hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(1024), 0, s, ptrack, n, tomb, n_tracks, cnt);
+    launch_scan(cnt, off, nb, tmp, s);
+    hipLaunchKernelGGL(k_compact_scatter, dim3((unsigned)nb), dim3(1024), 0, s, ph, ptrack, pt, n, tomb, n_tracks, off,
+                       oh, otrack, ot);
+}
+
 // extracted records of clip c -> postings (hash, track_ids[c], t) at dst_off[c]
 __global__ void k_records_to_postings(const uint64_t *__restrict__ recs, const int64_t *__restrict__ src_off,
                                       const int64_t *__restrict__ counts, const int64_t *__restrict__ dst_off,

@@ -146,8 +146,15 @@ int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids);
 /* Add n postings (hash, track, t) from host (AID_PCM_HOST) or device (AID_PCM_DEVICE) arrays. */
 int aid_index_add_postings(aid_engine *e, const uint32_t *hash, const uint32_t *track, const uint32_t *t, int64_t n,
                            int32_t location);
+/* Register track id `track` without postings (a clip too short or too quiet to give a hash), so a
+ * later aid_index_remove of it succeeds like `olaf_c del` of any stored name (fingerprint.py:239-262).
+ * Idempotent. */
+int aid_index_add_track(aid_engine *e, uint32_t track);
 /* Tombstone a track: its postings stop voting; AID_ERR_INVALID if unknown or already removed. */
 int aid_index_remove(aid_engine *e, uint32_t track);
+/* Drop the stored postings of every removed track (order of the others kept; the LMDB delete of
+ * `olaf_c del` frees its entries). *n_removed = postings dropped. The CSR is rebuilt lazily. */
+int aid_index_compact(aid_engine *e, int64_t *n_removed);
 int aid_index_finalize(aid_engine *e);
 /* n_postings = stored postings, n_live = postings in the built CSR (-1 if stale), n_tracks = max id + 1 */
 int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks);

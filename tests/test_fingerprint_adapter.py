@@ -5,6 +5,8 @@ host logic runs without a GPU. The real engine path is covered by
 tests/test_gpu_adapter.py."""
 
 import asyncio
+import json
+import os
 import uuid
 
 import numpy as np
@@ -19,21 +21,29 @@ PCM = np.arange(4000, dtype="<f4").tobytes()
 
 
 class FakeEngine:
-    """Test double of aidfp.engine.Engine: 'fingerprints' are the first PCM values."""
+    """Test double of aidfp.engine.Engine: 'fingerprints' are the first PCM values, carried in
+    the records (so a journal replay restores them); save/load keep the live state as JSON."""
+
+    fail_load = False  # class-wide: the next engine's index_load raises (truncated file, OOM ...)
+    saved_bytes = 0    # bytes written by index_save, all engines
 
     def __init__(self, sample_rate, device=-1, fail=None):
         self.sample_rate, self.hop = sample_rate, 256
         self.tracks, self.removed, self.fail = {}, set(), fail
-        self._last = None
+        self.closed = False
 
     def extract_host(self, clips):
         if self.fail == "extract":
             raise _lib.EngineError(-1, "bad input")
         self._last = [np.asarray(c[:3], dtype=np.float32) for c in clips]
-        return [np.arange(3, dtype=np.uint64) for _ in clips]
+        return [np.asarray(c[:3], dtype=np.float32).view(np.uint32).astype(np.uint64) for c in clips]
 
     def index_add_records(self, track, recs):
-        self.tracks[track] = self._last[0]
+        self.tracks[track] = np.asarray(recs, dtype=np.uint64).astype(np.uint32).view(np.float32)
+
+    def index_compact(self):
+        n = sum(len(self.tracks.pop(t)) for t in list(self.removed) if t in self.tracks)
+        return n
 
     def index_remove(self, track):
         if track in self.removed or track not in self.tracks:
@@ -47,13 +57,20 @@ class FakeEngine:
         return [np.array(rows, dtype=np.int64).reshape(-1, 5)]
 
     def index_save(self, path):
-        open(path, "w").write("x")
+        blob = json.dumps({"tracks": {str(t): v.tolist() for t, v in self.tracks.items()},
+                           "removed": sorted(self.removed)})
+        open(path, "w").write(blob)
+        FakeEngine.saved_bytes += len(blob)
 
     def index_load(self, path):
-        pass
+        if FakeEngine.fail_load:
+            raise _lib.EngineError(-2, "truncated index file")
+        d = json.loads(open(path).read())
+        self.tracks = {int(t): np.asarray(v, dtype=np.float32) for t, v in d["tracks"].items()}
+        self.removed = set(d["removed"])
 
     def close(self):
-        pass
+        self.closed = True
 
 
 @pytest.fixture
@@ -78,7 +95,9 @@ def test_index_empty_pcm_returns_false(svc):
 
 def test_index_success_persists(svc, tmp_path):
     assert run(fp.olaf_index_track(PCM, TID)) is True
-    assert (tmp_path / "db" / "index.aidfp").exists() and (tmp_path / "db" / "tracks.json").exists()
+    assert (tmp_path / "db" / "journal.0.aidfj").exists()  # one journal entry, no full rewrite
+    again = fp.FingerprintService(tmp_path / "db")  # a restart replays it
+    assert again.query(PCM)[0].reference_path == str(TID)
 
 
 def test_index_engine_error_returns_false(svc):
@@ -148,3 +167,156 @@ def test_cli_shim_roundtrip(tmp_path, monkeypatch, capsys):
     assert isinstance(parsed, list)
     assert cli.main(["del", "not-there"]) == 1
     assert cli.main(["bogus"]) == 2
+
+
+# ---------------------------------------------------------------- persistence (aidfp.store)
+
+def _svc(path, **kw):
+    return fp.FingerprintService(path, **kw)
+
+
+@pytest.fixture
+def fake_engine(monkeypatch):
+    import aidfp.engine as E
+
+    monkeypatch.setattr(E, "Engine", FakeEngine)
+    FakeEngine.fail_load = False
+    FakeEngine.saved_bytes = 0
+    yield FakeEngine
+    FakeEngine.fail_load = False
+
+
+def _pcm(i):
+    return np.array([i, i + 0.5, -i, 7], dtype="<f4").tobytes()
+
+
+def test_failed_load_never_overwrites_the_catalog(fake_engine, tmp_path):
+    """a failed index load must not let the next store replace the saved catalog."""
+    db = tmp_path / "db"
+    s = _svc(db, checkpoint_min_bytes=0)  # checkpoint on every write: a snapshot exists
+    a, b, c = (str(uuid.UUID(int=i)) for i in (1, 2, 3))
+    assert s.index_track(_pcm(1), a) and s.index_track(_pcm(2), b)
+    s.close()
+    before = {p.name: p.read_bytes() for p in db.iterdir()}
+    fake_engine.fail_load = True
+    s2 = _svc(db, checkpoint_min_bytes=0)
+    with pytest.raises(fp.OlafError, match="cannot load"):
+        s2.index_track(_pcm(3), c)
+    assert s2._engine is None
+    with pytest.raises(fp.OlafError):  # every later call retries the load, none writes
+        s2.delete_track(a)
+    assert {p.name: p.read_bytes() for p in db.iterdir()} == before
+    fake_engine.fail_load = False
+    assert s2.index_track(_pcm(3), c)  # the load succeeds now: the catalog is {a, b, c}
+    s3 = _svc(db)
+    s3._eng()
+    assert sorted(s3._ids) == sorted([a, b, c])
+
+
+def test_journal_replay_restores_stores_and_deletes(fake_engine, tmp_path):
+    db = tmp_path / "db"
+    s = _svc(db)
+    names = [str(uuid.UUID(int=i)) for i in range(6)]
+    for i, n in enumerate(names):
+        assert s.index_track(_pcm(i), n)
+    assert s.delete_track(names[1])
+    assert s.index_track(_pcm(40), names[2])  # re-store replaces
+    ids, nxt = dict(s._ids), s._next
+    s.close()
+    r = _svc(db)
+    r._eng()
+    assert r._ids == ids and r._next == nxt
+    assert r.query(_pcm(40))[0].reference_path == names[2]
+    assert all(m.reference_path != names[1] for m in r.query(_pcm(1)))
+
+
+def test_torn_journal_tail_is_dropped(fake_engine, tmp_path):
+    db = tmp_path / "db"
+    s = _svc(db)
+    assert s.index_track(_pcm(1), "a") and s.index_track(_pcm(2), "b")
+    s.close()
+    j = db / "journal.0.aidfj"
+    good = j.stat().st_size
+    with open(j, "ab") as f:  # a crash in the middle of a third append
+        f.write(b"AIDJ\x01\x00\x00\x00garbage")
+    r = _svc(db)
+    r._eng()
+    assert sorted(r._ids) == ["a", "b"]
+    assert j.stat().st_size == good
+    assert r.index_track(_pcm(3), "c")  # appends continue after the repaired tail
+    r2 = _svc(db)
+    r2._eng()
+    assert sorted(r2._ids) == ["a", "b", "c"]
+
+
+def test_checkpoint_compacts_and_crash_keeps_old_generation(fake_engine, tmp_path, monkeypatch):
+    db = tmp_path / "db"
+    s = _svc(db, checkpoint_min_bytes=1 << 30)
+    for i in range(4):
+        assert s.index_track(_pcm(i), f"t{i}")
+    assert s.delete_track("t0")
+    s.checkpoint()
+    assert json.loads((db / "tracks.json").read_text())["gen"] == 1
+    assert 0 not in s._engine.tracks  # removed postings compacted before the snapshot
+    assert not (db / "journal.0.aidfj").exists()
+    assert s.index_track(_pcm(9), "t9")
+    # a crash inside the next checkpoint, after the snapshot write, before the manifest commit
+    real_replace = os.replace
+
+    def crash(src, dst):
+        if str(dst).endswith("tracks.json"):
+            raise OSError("power cut")
+        return real_replace(src, dst)
+
+    monkeypatch.setattr(os, "replace", crash)
+    with pytest.raises(OSError):
+        s.checkpoint()
+    monkeypatch.setattr(os, "replace", real_replace)
+    r = _svc(db)
+    r._eng()
+    assert sorted(r._ids) == ["t1", "t2", "t3", "t9"]  # generation 1 + its journal
+
+
+def test_ingest_bytes_grow_linearly(fake_engine, tmp_path):
+    """N stores must not rewrite the whole index each time (O(N^2) bytes)."""
+    db = tmp_path / "db"
+    s = _svc(db, checkpoint_min_bytes=4096)
+    n = 400
+    for i in range(n):
+        assert s.index_track(_pcm(i), f"track-{i}")
+    journal = s._store.journal_bytes
+    snap_bytes = FakeEngine.saved_bytes
+    final = (db / s._store.snapshot).stat().st_size if s._store.snapshot else 0
+    # every checkpoint at least doubles the bytes it folds in: snapshots total < 2x the final one
+    assert snap_bytes <= 2 * final + 4096
+    assert journal <= max(4096, final) + 200
+    r = _svc(db)
+    r._eng()
+    assert len(r._ids) == n
+
+
+def test_zero_hash_track_delete_and_restore(fake_engine, tmp_path):
+    """a clip with no hashes still gets an id that can be deleted and re-stored."""
+    s = _svc(tmp_path / "db")
+    short = np.zeros(0, dtype="<f4").tobytes() + np.zeros(1, dtype="<f4").tobytes()
+    assert s.index_track(short, "tiny")
+    assert s.delete_track("tiny")
+    assert s.index_track(short, "tiny") and s.index_track(short, "tiny")
+
+
+def test_exact_lane_engine_unavailable_returns_empty(tmp_path, monkeypatch):
+    """the reference's exact lane logs an OlafError and returns [] (exact.py:163-171)."""
+    import aidfp.engine as E
+    from aidfp import exact
+
+    def boom(*a, **k):
+        raise _lib.EngineUnavailable("libaidfp.so missing")
+
+    monkeypatch.setattr(E, "Engine", boom)
+    fp.set_service(fp.FingerprintService(tmp_path))
+    try:
+        got = run(exact.run_exact_lane_batch([PCM, PCM], 5, lookup=lambda ids: {}))
+        assert got == [[], []]
+        assert run(exact.run_exact_lane(PCM, 5)) == []
+    finally:
+        fp.set_service(None)

@@ -70,3 +70,27 @@ def test_delete_and_reload(service):
         assert all(m.reference_path != str(IDS[5]) for m in other.query(pcm_bytes(5, 10.0, 6.0)))
     finally:
         other.close()
+
+
+def test_short_clip_store_delete_restore(tmp_path):
+    """a clip shorter than one frame (2048 samples) gives no hashes; it is still
+    stored, deletable and re-storable through the real engine, and survives a restart."""
+    svc = fp.FingerprintService(tmp_path / "db")
+    tid = uuid.UUID(int=0xBEEF)
+    short = np.full(1500, 0.1, dtype="<f4").tobytes()
+    try:
+        assert svc.index_track(short, str(tid))
+        assert svc.delete_track(str(tid))
+        assert svc.index_track(short, str(tid))
+        assert svc.index_track(short, str(tid))  # re-store over a zero-hash track
+        assert svc.index_track(pcm_bytes(4, 0, 20), "full")
+        svc.checkpoint()  # snapshot + compaction of the replaced ids
+    finally:
+        svc.close()
+    again = fp.FingerprintService(tmp_path / "db")
+    try:
+        assert again.delete_track(str(tid))
+        r = again.query(pcm_bytes(4, 6.0, 6.0))
+        assert r and r[0].reference_path == "full"
+    finally:
+        again.close()

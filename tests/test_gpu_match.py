@@ -108,3 +108,86 @@ def test_empty_index_and_empty_query():
         eng.index_finalize()
         out = eng.query([np.zeros(0, np.uint64), O.fingerprint(synth.synth(1, 0, 16000 * 4, 16000), 256)])
         assert [len(o) for o in out] == [0, 0]
+
+
+def _small_catalog(eng, n_tracks=6, seconds=12, sr=16000):
+    import torch
+
+    n = sr * seconds
+    pcm = torch.empty(n_tracks * n, dtype=torch.float32, device="cuda")
+    tracks = np.arange(n_tracks, dtype=np.uint32) + 10
+    eng.synth(pcm.data_ptr(), tracks, np.zeros(n_tracks, np.int64), n)
+    eng.extract_device(pcm.data_ptr(), np.arange(n_tracks + 1, dtype=np.int64) * n)
+    eng.index_add_extracted(tracks)
+    torch.cuda.synchronize()
+    return tracks
+
+
+def test_compact_drops_removed_postings_in_order(tmp_path):
+    """aid_index_compact (removed tracks' postings were never reclaimed): the stored
+    postings become exactly the live ones, in their order, and query rows do not change."""
+    sr, hop = 16000, 256
+    with Engine(sr) as eng:
+        tracks = _small_catalog(eng)
+        before = eng.index_export()
+        q = [O.fingerprint(synth.synth(int(t), sr * 3, sr * 4, sr, snr_db=20.0, salt=5), hop) for t in tracks[:4]]
+        for victim in (tracks[1], tracks[4]):
+            eng.index_remove(int(victim))
+        rows_before = eng.query(q)
+        dropped = eng.index_compact()
+        after = eng.index_export()
+        keep = ~np.isin(before[:, 1], [tracks[1], tracks[4]])
+        assert dropped == int((~keep).sum()) > 0
+        assert np.array_equal(after, before[keep])
+        rows_after = eng.query(q)
+        for a, b, r in zip(rows_before, rows_after, q):
+            assert np.array_equal(a, b)
+            assert np.array_equal(b, O.query(after, r, min_match=eng.min_match, max_rows=eng.max_results))
+        assert eng.index_compact() == 0  # nothing left to drop
+        with pytest.raises(Exception):
+            eng.index_remove(int(tracks[1]))  # still removed (tombstones survive compaction)
+
+
+def test_failed_load_leaves_the_index_untouched(tmp_path):
+    """aid_index_load validates the file and reads it into scratch buffers first; a
+    bad or truncated file fails without changing the loaded index."""
+    sr, hop = 16000, 256
+    with Engine(sr) as eng:
+        _small_catalog(eng, n_tracks=3)
+        good = tmp_path / "good.aidfp"
+        eng.index_save(str(good))
+        post = eng.index_export()
+        st = eng.index_stats()
+        q = [O.fingerprint(synth.synth(11, sr * 2, sr * 4, sr), hop)]
+        rows = eng.query(q)
+        blob = good.read_bytes()
+        bad = {
+            "truncated": blob[: len(blob) - 5],
+            "trailing": blob + b"\0",
+            "magic": b"XXXXXXXX" + blob[8:],
+            "abi": blob[:8] + np.int64(99).tobytes() + blob[16:],
+            "negative": blob[:32] + np.int64(-1).tobytes() + blob[40:],
+        }
+        for what, data in bad.items():
+            p = tmp_path / f"{what}.aidfp"
+            p.write_bytes(data)
+            with pytest.raises(Exception):
+                eng.index_load(str(p))
+            assert eng.index_stats()["postings"] == st["postings"], what
+            assert np.array_equal(eng.index_export(), post), what
+            assert all(np.array_equal(a, b) for a, b in zip(eng.query(q), rows)), what
+        with Engine(sr) as e2:
+            e2.index_load(str(good))
+            assert np.array_equal(e2.index_export(), post)
+
+
+def test_zero_hash_track_has_a_slot():
+    """a track with no hashes (shorter than one frame) can be removed after it is added."""
+    with Engine(16000) as eng:
+        recs = eng.extract_host([np.zeros(1000, np.float32)])[0]
+        assert len(recs) == 0
+        eng.index_add_records(77, recs)
+        assert eng.index_stats()["tracks"] == 78
+        eng.index_remove(77)
+        with pytest.raises(Exception):
+            eng.index_remove(77)
