@@ -49,6 +49,11 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_DIAG
 #define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
 #endif
+#ifndef AID_K2_NBUF
+#define AID_K2_NBUF 1  // row staging buffers: 2 = double-buffered (42 KB LDS: 3 workgroups per CU),
+                       // 1 = single buffer + a second barrier per 4 rows (21 KB: 4 per CU, VGPR-bound):
+                       // K2 0.1908 -> 0.1692 ms, 4.86 -> 5.07 M audio-s/s (same-box A/B, r02)
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
@@ -67,9 +72,9 @@ __device__ __forceinline__ int pkey(float x) {
 __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
                                                   const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask) {
-    __shared__ __attribute__((aligned(16))) int rows[2][kRowsPerStep][kBins + 32];
+    __shared__ __attribute__((aligned(16))) int rows[AID_K2_NBUF][kRowsPerStep][kBins + 32];
 #if AID_K2_BLOCKMAX
-    __shared__ __attribute__((aligned(16))) int bms[2][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
+    __shared__ __attribute__((aligned(16))) int bms[AID_K2_NBUF][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
 #endif
     // wave = the 256-bin quarter of the row this wave owns, rotated by the workgroup index: the
     // waves of a workgroup go to the CU's 4 SIMDs in order, so without rotation every workgroup's
@@ -110,7 +115,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 
     if (tid < 16) {
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < AID_K2_NBUF; ++b)
 #pragma unroll
             for (int r = 0; r < kRowsPerStep; ++r) {
                 rows[b][r][tid] = 0;
@@ -171,8 +176,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
         for (int s = 0; s < 8; ++s) {
             const int it = base + s;
             if (it >= iters) break;  // workgroup-uniform
-            const int buf = (it / kRowsPerStep) & 1;
+            const int buf = AID_K2_NBUF == 1 ? 0 : (it / kRowsPerStep) & 1;
             if (AID_K2_DIAG != 2 && s % kRowsPerStep == 0) {
+                if (AID_K2_NBUF == 1 && it > 0) __syncthreads();  // every wave is done with the previous 4 rows
                 // stage rows it .. it+3 as keys, then fetch rows it+PF .. (register staging beats
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll

@@ -101,6 +101,81 @@ __device__ __forceinline__ float quad_dpp(float x) {
 __device__ __forceinline__ int e3(int k) { return k ^ (((k >> 4) & 3) << 2); }
 #endif
 
+// AID_K1_E1SWAP=1: E1 as an in-register transpose of (register k1) x (lane bits 2-5 = m1): register
+// bit s is exchanged with lane bit 2+s, s = 3 and 2 by v_permlane32/16_swap (one instruction moves one
+// float of two registers), s = 1 and 0 by DPP v_cndmask (row_shr/row_shl by 8 / 4 lanes inside a
+// row, two instructions per float pair). No LDS, no wait; 96 VALU instead of 16 ds_write_b64 +
+// 8 ds_read_b128. Pure data movement: the values are bit-identical to the LDS exchange.
+#ifndef AID_K1_E1SWAP
+#define AID_K1_E1SWAP 0
+#endif
+#if AID_K1_E1SWAP
+__device__ __forceinline__ void lane_swap32(float &a, float &b) {  // a[32+i] <-> b[i]
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void lane_swap16(float &a, float &b) {  // a[odd row] <-> b[even row]
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+// Exchange across lane bit log2(D) (D = 4 or 8, inside a row of 16) for two register pairs (a_i, b_i):
+//   a'[l] = bit ? b[l - D] : a[l] ;  b'[l] = bit ? b[l] : a[l + D]
+// v_cndmask_b32 (VOP2 + DPP on src0): D = vcc ? src1 : dpp(src0). bound_ctrl:0 zero-fills the source of
+// the lanes whose partner is outside the row; those lanes select src1 anyway.
+#define AID_XCHG_ASM(SHR, SHL)                                                            \
+    "s_mov_b64 vcc, %[nm]\n\t"                                                            \
+    "s_nop 1\n\t"                                                                         \
+    "v_cndmask_b32_dpp %0, %12, %8, vcc " SHR " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"  \
+    "v_cndmask_b32_dpp %1, %13, %9, vcc " SHR " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"  \
+    "v_cndmask_b32_dpp %2, %14, %10, vcc " SHR " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t" \
+    "v_cndmask_b32_dpp %3, %15, %11, vcc " SHR " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t" \
+    "s_mov_b64 vcc, %[m]\n\t"                                                             \
+    "v_cndmask_b32_dpp %4, %8, %12, vcc " SHL " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"  \
+    "v_cndmask_b32_dpp %5, %9, %13, vcc " SHL " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t"  \
+    "v_cndmask_b32_dpp %6, %10, %14, vcc " SHL " row_mask:0xf bank_mask:0xf bound_ctrl:0\n\t" \
+    "v_cndmask_b32_dpp %7, %11, %15, vcc " SHL " row_mask:0xf bank_mask:0xf bound_ctrl:0"
+template <int D>
+__device__ __forceinline__ void lane_xchg(float2 &a0, float2 &b0, float2 &a1, float2 &b1) {
+    // nm = lanes with the exchanged bit CLEAR (they keep a), m = lanes with it set (they keep b). Only
+    // s_mov touches scalar state here: an s_not would write SCC, which the compiler may hold live
+    // between the halves of a 64-bit s_add_u32/s_addc_u32 around this block (it did: a wrong address).
+    constexpr unsigned long long nm = D == 4 ? 0x0F0F0F0F0F0F0F0Full : 0x00FF00FF00FF00FFull;
+    constexpr unsigned long long m = ~nm;
+    float o[8];
+#define AID_XCHG_OPERANDS                                                                               \
+    : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7]) \
+    : "v"(a0.x), "v"(a0.y), "v"(a1.x), "v"(a1.y), "v"(b0.x), "v"(b0.y), "v"(b1.x), "v"(b1.y), [nm] "s"(nm), [m] "s"(m) \
+    : "vcc"
+    if constexpr (D == 4) asm volatile(AID_XCHG_ASM("row_shr:4", "row_shl:4") AID_XCHG_OPERANDS);
+    else asm volatile(AID_XCHG_ASM("row_shr:8", "row_shl:8") AID_XCHG_OPERANDS);
+#undef AID_XCHG_OPERANDS
+    a0 = make_float2(o[0], o[1]);
+    a1 = make_float2(o[2], o[3]);
+    b0 = make_float2(o[4], o[5]);
+    b1 = make_float2(o[6], o[7]);
+}
+// E1 transpose: in lane n2 = 4 m1 + m2, v[k1] = A[k1][n2]; out in lane 4 k1 + m2, v[m1] = A[k1][4 m1 + m2]
+__device__ __forceinline__ void e1_transpose(float2 (&v)[16]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {  // register bit 3 <-> lane bit 5
+        lane_swap32(v[r].x, v[r + 8].x);
+        lane_swap32(v[r].y, v[r + 8].y);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r)  // register bit 2 <-> lane bit 4
+        if (!(r & 4)) {
+            lane_swap16(v[r].x, v[r + 4].x);
+            lane_swap16(v[r].y, v[r + 4].y);
+        }
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) lane_xchg<8>(v[r], v[r + 2], v[r + 1], v[r + 3]);  // bit 1 <-> lane bit 3
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) lane_xchg<4>(v[r], v[r + 1], v[r + 2], v[r + 3]);  // bit 0 <-> lane bit 2
+}
+#endif
+
 template <bool LOGMAG, int ROWS>
 __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
@@ -251,7 +326,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
                 if (AID_K1_DIAG != 6) {
-#if AID_K1_E1V
+#if AID_K1_E1SWAP
+                    e1_transpose(v);
+#elif AID_K1_E1V
 #pragma unroll
                     for (int k1 = 0; k1 < 16; ++k1)
                         buf[k1 * 64 + 8 * ((kq >> 1) ^ (k1 & 7)) + 2 * mq + (kq & 1)] = v[k1];
@@ -274,7 +351,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                     : AID_K1_COMPACT ? kq * 64 + 4 * ((m1 & 8) | ((m1 ^ kq) & 7)) + mq
                                                      : kq * 68 + 4 * m1 + mq];
 #endif
-                    wave_lds_sync();
+                    if (!AID_K1_E1SWAP) wave_lds_sync();
                 }
                 // stage B
 #if AID_K1_PRIO
