@@ -304,7 +304,10 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     if (c.hop != 128 && c.hop != 256 && c.hop != 512 && c.hop != 1024 && c.hop != 2048)
         return fail(AID_ERR_INVALID, "hop must be one of 128, 256, 512, 1024, 2048");
     if (c.peak_threshold == 0.0f) c.peak_threshold = 4.0f;
-    if (!(c.peak_threshold > 0.0f)) return fail(AID_ERR_INVALID, "peak_threshold must be > 0");
+    // [2^-124, 2^100]: K1/K2 compare the plane's Q = 4P against 4 thr. In that range 4 thr is exact and
+    // any Q of a candidate (Q > 4 thr) is normal, so Q-order and P-order decide every comparison alike
+    if (!(c.peak_threshold >= 0x1p-124f) || c.peak_threshold > 0x1p100f)
+        return fail(AID_ERR_INVALID, "peak_threshold must be in [2^-124, 2^100]");
     if (c.min_match <= 0) c.min_match = 12;
     if (c.max_results <= 0) c.max_results = 50;
     if (c.flags & ~AID_FLAG_KEEP_POWER) return fail(AID_ERR_INVALID, "unknown aid_config.flags bits");
@@ -643,6 +646,8 @@ int aid_result_power(aid_engine *e, int32_t clip, float *out, int64_t cap) {
         int64_t fb = 0;
         for (int c = 0; c < clip; ++c) fb += e->clip_frames[c];
         HIP_TRY(hipMemcpy(out, e->power.p + fb * kBins, F * kBins * sizeof(float), hipMemcpyDeviceToHost));
+        // K1 stores Q = fma(Xr, Xr, Xi*Xi) = 4P; FPSPEC 4's P is Q * 0.25f, the same binary32 op
+        for (int64_t i = 0; i < F * kBins; ++i) out[i] = out[i] * 0.25f;
     }
     return AID_OK;
 }

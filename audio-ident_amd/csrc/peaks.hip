@@ -59,7 +59,7 @@ constexpr int kRowsPerStep = 4;
 #endif
 
 // Peak decisions compare powers as int32 keys: a power is >= +0 (never -0: FPSPEC 4's
-// fma(Xr, Xr, Xi*Xi) * 0.25f), and non-negative binary32 values order exactly like their bit
+// fma(Xr, Xr, Xi*Xi), stored unscaled as 4P by K1), and non-negative binary32 values order exactly like their bit
 // patterns. NaN maps to key 0, which reproduces the oracle's `row > l ? row : l` maxima (a NaN
 // neighbour never raises a maximum) and `!(p > thr)` (a NaN is never a peak); +inf keeps its
 // bits. Integer max needs no NaN canonicalisation: hipcc put a `v_max_f32 x, x, x` in front of
@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     const int t1 = min(t0 + strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
-    const int kthr = __float_as_int(thr);                   // thr > 0 (engine config check)
+    // K1's plane holds Q = 4P (stft.hip, real split): compare against 4 thr (exact: thr <= 2^100)
+    const int kthr = __float_as_int(4.0f * thr);            // thr > 0 (engine config check)
 
     if (tid < 16) {
 #pragma unroll

@@ -498,7 +498,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     {
                         const float2 tw = cmul(make_float2(orr, oi), make_float2(t2.x, t2.y));
                         const float xr = er + tw.x, xi = ei + tw.y;
-                        const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                        // FPSPEC 4: P = fma(..) * 0.25f. The plane stores Q = fma(..) = 4P instead (one
+                        // VALU less per bin): the scaling by 4 is exact and order-preserving, so every
+                        // decision against thr is the same against 4 thr (the caller passes 4 thr), and
+                        // aid_result_power applies the spec's * 0.25f on readout (bit-identical P)
+                        const float P = LOGMAG ? __builtin_fmaf(xr, xr, xi * xi) * 0.25f : __builtin_fmaf(xr, xr, xi * xi);
                         const uint64_t hd = LOGMAG ? 0 : __ballot(P > thr);
                         if constexpr (LOGMAG) drow[k] = 10.0f * log10f(P + 1e-10f);
                         else if (AID_K1_DIAG == 10) acc10 += P;
@@ -510,7 +514,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     if (k != 0) {  // bin 1024-k (513..1023); k = 0's mirror is the dropped Nyquist bin
                         const float2 tw = cmul(make_float2(orr, -oi), make_float2(t2.z, t2.w));
                         const float xr = er + tw.x, xi = -ei + tw.y;
-                        const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                        const float P = LOGMAG ? __builtin_fmaf(xr, xr, xi * xi) * 0.25f : __builtin_fmaf(xr, xr, xi * xi);
                         if constexpr (LOGMAG) drow[1024 - k] = 10.0f * log10f(P + 1e-10f);
                         else if (AID_K1_DIAG == 10) acc10 += P;
                         else if (AID_K1_DIAG == 11) pv11[2 * i + 1] = P;
@@ -538,7 +542,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
                     const float2 tw = cmul(make_float2(orr, oi), t512);
                     const float xr = er + tw.x, xi = ei + tw.y;
-                    const float P = __builtin_fmaf(xr, xr, xi * xi) * 0.25f;
+                    const float P = LOGMAG ? __builtin_fmaf(xr, xr, xi * xi) * 0.25f : __builtin_fmaf(xr, xr, xi * xi);
                     if constexpr (LOGMAG) drow[512] = 10.0f * log10f(P + 1e-10f);
                     else drow[512] = P;
                     if (P > thr) hotw |= 1u << 8;
@@ -593,7 +597,9 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
 #endif
     const dim3 g((unsigned)((n_waves + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
     if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr, 1);
-    else launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep_power ? 1 : 0);
+    else  // the power plane holds 4P (see the real split): hot blocks are those with 4P > 4 thr
+        launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, 4.0f * thr,
+                           keep_power ? 1 : 0);
 }
 
 }  // namespace aid

@@ -54,7 +54,7 @@ typedef struct aid_engine aid_engine;
 typedef struct aid_config {
     int32_t sample_rate;   /* Hz; per-index property */
     int32_t hop;           /* 0 = FPSPEC default: 512 at sr >= 32 kHz, else 256 */
-    float peak_threshold;  /* 0 = FPSPEC default 4.0 */
+    float peak_threshold;  /* 0 = FPSPEC default 4.0; otherwise in [2^-124, 2^100] */
     int32_t device;        /* HIP device ordinal; -1 = current device */
     int32_t min_match;     /* query: 0 = FPSPEC default 12 */
     int32_t max_results;   /* query: 0 = FPSPEC default 50 */
