@@ -21,6 +21,7 @@ constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 #endif
 constexpr int kStftWaves = AID_STFT_WAVES;
 constexpr int kStftStrip = 16;
+constexpr int kK1DummyRows = 256;  // K1 cold-block store sinks (one 8 KB row per workgroup index mod 256)
 #ifndef AID_K1_COMPACT
 #define AID_K1_COMPACT 1
 #endif

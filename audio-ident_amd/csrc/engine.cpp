@@ -24,7 +24,7 @@
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, bool keep_power, hipStream_t s);
+                       uint32_t *hot, float thr, bool keep_power, float *dummy, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
                       const uint32_t *hot, uint64_t *mask, hipStream_t s);
@@ -131,6 +131,7 @@ struct aid_engine {
     DevBuf<float> power;
     DevBuf<uint64_t> mask;
     DevBuf<uint32_t> hotw;  // K1 -> K2: per power row, bit b = 64-bin block b has a value > thr
+    DevBuf<float> k1_dummy;  // K1's sink for cold-block stores: kK1DummyRows x 2048 floats
     DevBuf<ClipDesc> desc;
     DevBuf<int64_t> chunk_counts;
     DevBuf<uint64_t> records;
@@ -380,6 +381,7 @@ void aid_engine_destroy(aid_engine *e) {
     for (auto ev : e->pool) (void)hipEventDestroy(ev);
     e->pcm_stage.release();
     e->power.release();
+    e->k1_dummy.release();
     e->mask.release();
     e->desc.release();
     e->chunk_counts.release();
@@ -525,6 +527,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     HIP_TRY(e->power.reserve((size_t)frames * kBins));
     HIP_TRY(e->mask.reserve((size_t)frames * kMaskWords));
     HIP_TRY(e->hotw.reserve((size_t)frames + 1));
+    HIP_TRY(e->k1_dummy.reserve((size_t)kK1DummyRows * 2048));
     HIP_TRY(e->chunk_counts.reserve((size_t)chunks + 1));
     HIP_TRY(e->records.reserve((size_t)recs + 1));
     HIP_TRY(e->counts.reserve((size_t)n_clips + 1));
@@ -562,7 +565,8 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         {
             ProfScope ps(e, AID_K_STFT, s, true);
             launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false,
-                              e->hotw.p, e->cfg.peak_threshold, (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0, s);
+                              e->hotw.p, e->cfg.peak_threshold, (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0,
+                              e->k1_dummy.p, s);
         }
         if (loc == AID_PCM_HOST) {
             if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
@@ -687,7 +691,7 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
         launch_stft_power(d_pcm, d_desc, 1, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
-                          d_out, true, nullptr, e->cfg.peak_threshold, true, s);
+                          d_out, true, nullptr, e->cfg.peak_threshold, true, nullptr, s);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);

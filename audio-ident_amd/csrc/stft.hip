@@ -75,6 +75,13 @@
 #ifndef AID_K1_E1V
 #define AID_K1_E1V 1
 #endif
+// AID_K1_BRANCHFREE=1: the real split computes the row's 16 powers per lane first, then the hot word,
+// then stores all 16 unconditionally, a cold block's into a per-workgroup dummy row (scalar base
+// select). The guarded stores of the earlier code put a scalar branch after every bin pair, which
+// cut the split into 16 short blocks the compiler could not interleave.
+#ifndef AID_K1_BRANCHFREE
+#define AID_K1_BRANCHFREE 1  // K1 0.2935 -> 0.2863 ms same-box (r02)
+#endif
 // AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
 // (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
 
@@ -181,7 +188,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
                                                                 int64_t total, int64_t n_waves,
                                                                 const Tables *__restrict__ tab, float *__restrict__ out,
-                                                                uint32_t *__restrict__ hot, float thr, int keep) {
+                                                                uint32_t *__restrict__ hot, float thr, int keep,
+                                                                float *__restrict__ dummy_rows) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ __attribute__((aligned(16))) float2 lds[kStftWaves][kStftLdsPerWave];  // E1: 16 x 68 (compact: 16 x 64), E2: 64 x 17 (16 x 64), E3: 1024
@@ -278,6 +286,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
     const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + lane;
     float *dst = out + (clips[lo].frame_base + t0) * kBins;
+    float *dummy = dummy_rows + (int64_t)(blockIdx.x & (kK1DummyRows - 1)) * 2048;  // cold-block store sink
     uint32_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
 
     float2 ring[16];
@@ -457,6 +466,65 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
                 wave_lds_sync();
                 float *drow = dst + (int64_t)f * kBins;
+#if AID_K1_BRANCHFREE
+                if constexpr (!LOGMAG && AID_K1_DIAG == 0) {
+                    // straight-line real split: all 16 powers first, then the hot word, then 16
+                    // unconditional stores whose base is the row or, for a cold block, this
+                    // workgroup's dummy row (a scalar select: no branch splits the arithmetic)
+                    uint32_t hotw = 0;
+                    float po[8], pm[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float2 a = buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
+                        const int bi = (i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
+                        const float2 bs = buf[bi];
+                        const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
+                        const float er = a.x + b.x, ei = a.y - b.y;
+                        const float orr = a.y + b.y, oi = b.x - a.x;
+                        const float2 t2h = s_t2[64 * i + lane];
+                        const float2 tw = cmul(make_float2(orr, oi), make_float2(t2h.x, t2h.y));
+                        const float xr = er + tw.x, xi = ei + tw.y;
+                        po[i] = __builtin_fmaf(xr, xr, xi * xi);  // Q = 4P (see below)
+                        const float2 tw2 = cmul(make_float2(orr, -oi), make_float2(-t2h.x, t2h.y));
+                        const float xr2 = er + tw2.x, xi2 = -ei + tw2.y;
+                        // k = 0 (lane 0, i = 0): the mirror is the dropped Nyquist bin
+                        pm[i] = (i == 0 && lane == 0) ? 0.f : __builtin_fmaf(xr2, xr2, xi2 * xi2);
+                        hotw |= __ballot(po[i] > thr) ? 1u << i : 0u;  // bins 64i..64i+63
+                        // lanes 1..63: bins of block 15 - i; lane 0 (i > 0): block 16 - i
+                        const uint64_t hb = __ballot(pm[i] > thr);
+                        hotw |= (hb >> 1) ? 1u << (15 - i) : 0u;
+                        hotw |= (hb & 1) ? 1u << (16 - i) : 0u;
+                    }
+                    float p512 = 0.f;
+                    if (lane == 0) {  // bin 512 pairs with itself
+                        const float2 a = buf[e3(512)];
+                        const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
+                        const float2 tw = cmul(make_float2(orr, oi), t512);
+                        const float xr = er + tw.x, xi = ei + tw.y;
+                        p512 = __builtin_fmaf(xr, xr, xi * xi);
+                        drow[512] = p512;
+                    }
+                    hotw |= __ballot(p512 > thr) ? 1u << 8 : 0u;
+                    if (lane == 0) dhot[f] = hotw;
+                    const uint32_t hsel = keep ? 0x1FFFFu : hotw;  // one select, not a branch per store
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        float *b = ((hsel >> i) & 1u) ? drow : dummy;
+                        b[lane + 64 * i] = po[i];
+                    }
+                    // mirror store i covers bins 1025-64(i+1) .. 1023-64i of block 15-i (lanes 1..63)
+                    // and bin 1024-64i of block 16-i (lane 0): written when either block is hot. A
+                    // skipped store leaves only bins of cold blocks stale, which K2 never reads.
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t need = (hsel >> (15 - i)) | (i > 0 ? hsel >> (16 - i) : 0u);
+                        float *b = (need & 1u) ? drow : dummy;
+                        if (i == 0) b = lane == 0 ? dummy : b;  // lane 0's mirror of k = 0 is not a bin
+                        b[1024 - (lane + 64 * i)] = pm[i];
+                    }
+                } else
+#endif
+                {
                 // hot blocks of the row: bit b = some bin of 64-bin block b is > thr (K2 skips the
                 // others: a value <= thr can neither be a peak nor suppress one, FPSPEC 5)
                 uint32_t hotw = 0;
@@ -559,6 +627,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         if ((keep || (need & 1u)) && (i > 0 || lane != 0)) drow[1024 - (lane + 64 * i)] = pm[i];
                     }
                 }
+                }
                 wave_lds_sync();
             }
         }
@@ -570,14 +639,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 }
 
 template <bool LOGMAG>
-static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
+static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, float *dummy, const float *pcm, const ClipDesc *clips, int n_clips,
                         int64_t total, int64_t n_waves, const Tables *tab, float *out, uint32_t *hot, float thr, int keep) {
     switch (rows) {
-        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
+        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep, dummy); break;
+        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep, dummy); break;
+        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep, dummy); break;
+        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep, dummy); break;
+        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep, dummy); break;
     }
 }
 
@@ -585,7 +654,7 @@ static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pc
 // slots = resident K1 waves on the device (CUs x kStftWaves)
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, bool keep_power, hipStream_t s) {
+                       uint32_t *hot, float thr, bool keep_power, float *dummy, hipStream_t s) {
     if (total_frames <= 0) return;
 #if AID_K1_BALANCED
     // one round of equal ranges; at least kStftStrip frames per wave (a ring fill per segment)
@@ -596,9 +665,9 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
     (void)slots;
 #endif
     const dim3 g((unsigned)((n_waves + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
-    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr, 1);
+    if (logmag) launch_rows<true>(hop / 128, g, b, s, dummy, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr, 1);
     else  // the power plane holds 4P (see the real split): hot blocks are those with 4P > 4 thr
-        launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, 4.0f * thr,
+        launch_rows<false>(hop / 128, g, b, s, dummy, pcm, clips, n_clips, total, n_waves, tab, out, hot, 4.0f * thr,
                            keep_power ? 1 : 0);
 }
 
