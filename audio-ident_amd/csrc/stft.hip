@@ -315,11 +315,13 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     v[2 * h] = make_float2(x0.x * w.x, x0.y * w.y);
                     v[2 * h + 1] = make_float2(x1.x * w.z, x1.y * w.w);
                 }
-                // the rows just consumed (n1 < ROWS) are replaced by frame f+1's new rows
-                if (f + 1 < nfr) {
+                // the rows just consumed (n1 < ROWS) are replaced by frame f+1's new rows (after the
+                // last frame of the segment: a harmless re-load of its own rows, instead of a branch)
+                {
+                    const int fn = min(f + 1, nfr - 1);
 #pragma unroll
                     for (int j = 0; j < ROWS; ++j)
-                        ring[(ROWS * p + j) & 15] = src[(int64_t)(f + 1) * HOP2 + 64 * (16 - ROWS + j)];
+                        ring[(ROWS * p + j) & 15] = src[(int64_t)fn * HOP2 + 64 * (16 - ROWS + j)];
                 }
                 // stage A: lane = n2
                 if (AID_K1_DIAG != 9) dft16(v, t16);
@@ -495,17 +497,18 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         hotw |= (hb >> 1) ? 1u << (15 - i) : 0u;
                         hotw |= (hb & 1) ? 1u << (16 - i) : 0u;
                     }
-                    float p512 = 0.f;
-                    if (lane == 0) {  // bin 512 pairs with itself
+                    {  // bin 512 pairs with itself: every lane computes it (same address, same value),
+                       // so its store and the hot word's need no lane-0 branch
                         const float2 a = buf[e3(512)];
                         const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
                         const float2 tw = cmul(make_float2(orr, oi), t512);
                         const float xr = er + tw.x, xi = ei + tw.y;
-                        p512 = __builtin_fmaf(xr, xr, xi * xi);
+                        const float p512 = __builtin_fmaf(xr, xr, xi * xi);
                         drow[512] = p512;
+                        hotw |= p512 > thr ? 1u << 8 : 0u;
                     }
-                    hotw |= __ballot(p512 > thr) ? 1u << 8 : 0u;
-                    if (lane == 0) dhot[f] = hotw;
+                    hotw = __builtin_amdgcn_readfirstlane(hotw);
+                    dhot[f] = hotw;
                     const uint32_t hsel = keep ? 0x1FFFFu : hotw;  // one select, not a branch per store
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
