@@ -21,7 +21,8 @@ constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 #endif
 constexpr int kStftWaves = AID_STFT_WAVES;
 constexpr int kStftStrip = 16;
-constexpr int kK1DummyRows = 256;  // K1 cold-block store sinks (one 8 KB row per workgroup index mod 256)
+constexpr int kK1DummyRows = 256;
+constexpr int kK2SinkBlocks = 1024;  // K2 mask-store sinks: 256 u64 per workgroup index mod 1024 (2 MB)  // K1 cold-block store sinks (one 8 KB row per workgroup index mod 256)
 #ifndef AID_K1_COMPACT
 #define AID_K1_COMPACT 1
 #endif

@@ -27,7 +27,7 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
                        uint32_t *hot, float thr, bool keep_power, float *dummy, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
-                      const uint32_t *hot, uint64_t *mask, hipStream_t s);
+                      const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink, hipStream_t s);
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
@@ -132,6 +132,8 @@ struct aid_engine {
     DevBuf<uint64_t> mask;
     DevBuf<uint32_t> hotw;  // K1 -> K2: per power row, bit b = 64-bin block b has a value > thr
     DevBuf<float> k1_dummy;  // K1's sink for cold-block stores: kK1DummyRows x 2048 floats
+    DevBuf<float> k2_zero;   // K2: a 1024-float zero row (cold-block loads)
+    DevBuf<uint64_t> k2_sink;  // K2: mask-store sink, kK2SinkBlocks x 256 words
     DevBuf<ClipDesc> desc;
     DevBuf<int64_t> chunk_counts;
     DevBuf<uint64_t> records;
@@ -382,6 +384,8 @@ void aid_engine_destroy(aid_engine *e) {
     e->pcm_stage.release();
     e->power.release();
     e->k1_dummy.release();
+    e->k2_zero.release();
+    e->k2_sink.release();
     e->mask.release();
     e->desc.release();
     e->chunk_counts.release();
@@ -528,6 +532,11 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     HIP_TRY(e->mask.reserve((size_t)frames * kMaskWords));
     HIP_TRY(e->hotw.reserve((size_t)frames + 1));
     HIP_TRY(e->k1_dummy.reserve((size_t)kK1DummyRows * 2048));
+    if (!e->k2_zero.p) {
+        HIP_TRY(e->k2_zero.reserve(kBins));
+        HIP_TRY(hipMemsetAsync(e->k2_zero.p, 0, kBins * sizeof(float), s));
+    }
+    HIP_TRY(e->k2_sink.reserve((size_t)kK2SinkBlocks * 256));
     HIP_TRY(e->chunk_counts.reserve((size_t)chunks + 1));
     HIP_TRY(e->records.reserve((size_t)recs + 1));
     HIP_TRY(e->counts.reserve((size_t)n_clips + 1));
@@ -576,7 +585,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         {
             ProfScope ps(e, AID_K_PEAKS, s, true);
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
-                             e->mask.p, s);
+                             e->mask.p, e->k2_zero.p, e->k2_sink.p, s);
         }
         if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s, true);

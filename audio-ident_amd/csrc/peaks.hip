@@ -54,6 +54,10 @@ constexpr int kRowsPerStep = 4;
                        // 1 = single buffer + a second barrier per 4 rows (21 KB: 4 per CU, VGPR-bound):
                        // K2 0.1908 -> 0.1692 ms, 4.86 -> 5.07 M audio-s/s (same-box A/B, r02)
 #endif
+#ifndef AID_K2_BRANCHFREE
+#define AID_K2_BRANCHFREE 0  // measured slower (K2 0.1709 -> 0.1789 ms: zero-row loads cost more than the branch). 1: row loads of cold blocks read a zero row and the mask store of other lanes/rows
+                             // goes to a dummy sink (per-lane address selects) instead of exec-masked branches
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
@@ -64,14 +68,26 @@ constexpr int kRowsPerStep = 4;
 // neighbour never raises a maximum) and `!(p > thr)` (a NaN is never a peak); +inf keeps its
 // bits. Integer max needs no NaN canonicalisation: hipcc put a `v_max_f32 x, x, x` in front of
 // ~19 of the ~65 fmaxf operands of every row.
+#ifndef AID_K2_FMAXKEY
+#define AID_K2_FMAXKEY 1  // K2 0.1709 -> 0.1623 ms same-box (r02). 1: the key is the bits of v_max_f32(0, x) (maxNum: a NaN gives 0, +-0 gives +0)
+#endif
 __device__ __forceinline__ int pkey(float x) {
+#if AID_K2_FMAXKEY
+    // one VALU instead of v_cmp + v_cndmask (+ the VCC hazard's s_nop). Same keys: the plane holds K1's
+    // fma results (quiet NaNs, no sNaN, no negative non-NaN values), and maxNum(qNaN, 0) = 0
+    float r;
+    asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+    return __float_as_int(r);
+#else
     const uint32_t b = __float_as_uint(x);
     return b <= 0x7F800000u ? (int)b : 0;
+#endif
 }
 
 __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
-                                                  const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask) {
+                                                  const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask,
+                                                  const float4 *__restrict__ zero_row, uint64_t *__restrict__ sink) {
     __shared__ __attribute__((aligned(16))) int rows[AID_K2_NBUF][kRowsPerStep][kBins + 32];
 #if AID_K2_BLOCKMAX
     __shared__ __attribute__((aligned(16))) int bms[AID_K2_NBUF][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
@@ -111,6 +127,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     const int t1 = min(t0 + strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
+    uint64_t *sinkw = sink + (int64_t)(blockIdx.x & (kK2SinkBlocks - 1)) * 256 + threadIdx.x;  // other stores
     // K1's plane holds Q = 4P (stft.hip, real split): compare against 4 thr (exact: thr <= 2^100)
     const int kthr = __float_as_int(4.0f * thr);            // thr > 0 (engine config check)
 
@@ -153,13 +170,26 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     // Words are fetched one step ahead of the row loads they gate (scalar loads)
     const uint32_t *HW = hot + fb;
     const int myb = tid >> 4;
+#if AID_K2_BRANCHFREE
+    // clamped scalar load + select: no branch around the s_load for rows outside the clip
+    auto hotword = [&](int r) -> uint32_t {
+        const uint32_t w = HW[min(max(r, 0), F - 1)];
+        return (r >= 0 && r < F) ? w : 0u;
+    };
+#else
     auto hotword = [&](int r) -> uint32_t { return (r >= 0 && r < F) ? HW[r] : 0u; };
+#endif
     float4 pf[AID_K2_PF];  // rows of the next batch(es), in flight
 #pragma unroll
     for (int j = 0; j < AID_K2_PF; ++j) {
         const int r = rbeg + j;
+#if AID_K2_BRANCHFREE
+        pf[j] = ((j < iters && ((hotword(r) >> myb) & 1u)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)
+                                                            : zero_row)[tid];
+#else
         pf[j] = (j < iters && ((hotword(r) >> myb) & 1u)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
                                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
     }
     uint32_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
 #pragma unroll
@@ -194,9 +224,16 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                     const int rn = rbeg + it + j + AID_K2_PF;
                     hcur[j] = hsave[j];
                     hsave[j] = hw[j];
+#if AID_K2_BRANCHFREE
+                    // a cold block (or a row past the strip) reads the zero row: one load per lane, no branch
+                    pf[slot] = ((it + j + AID_K2_PF < iters && ((hw[j] >> myb) & 1u))
+                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)
+                                    : zero_row)[tid];
+#else
                     pf[slot] = (it + j + AID_K2_PF < iters && ((hw[j] >> myb) & 1u))
                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
                     hw[j] = hotword(rn + kRowsPerStep);
                 }
                 __syncthreads();
@@ -321,19 +358,28 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             }
             const uint64_t b0 = __ballot(pk[0]), b1 = __ballot(pk[1]), b2 = __ballot(pk[2]), b3 = __ballot(pk[3]);
             const int rd = r - kPeakDT;
+#if AID_K2_BRANCHFREE
+            {
+                const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+                uint64_t *dstw = (rd >= t0 && rd < t1 && lane < 4) ? M + (int64_t)rd * kMaskWords : sinkw;
+                *dstw = wv;
+            }
+#else
             if (rd >= t0 && rd < t1 && lane < 4) {
                 const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
                 M[(int64_t)rd * kMaskWords] = wv;
             }
+#endif
         }
     }
 }
 
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
-                      float thr, const uint32_t *hot, uint64_t *mask, hipStream_t s) {
+                      float thr, const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink,
+                      hipStream_t s) {
     if (total_strips <= 0) return;
     timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
-                       strip_len, thr, hot, mask);
+                       strip_len, thr, hot, mask, reinterpret_cast<const float4 *>(zero_row), sink);
 }
 
 // resident K2 workgroups per CU (registers / LDS), for sizing strips to one round
