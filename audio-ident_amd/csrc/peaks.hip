@@ -127,7 +127,12 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     const int t1 = min(t0 + strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
+#if AID_K2_BRANCHFREE
     uint64_t *sinkw = sink + (int64_t)(blockIdx.x & (kK2SinkBlocks - 1)) * 256 + threadIdx.x;  // other stores
+#else
+    (void)sink;
+    (void)zero_row;
+#endif
     // K1's plane holds Q = 4P (stft.hip, real split): compare against 4 thr (exact: thr <= 2^100)
     const int kthr = __float_as_int(4.0f * thr);            // thr > 0 (engine config check)
 
@@ -264,6 +269,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             }
 #endif
             bool pk[4];
+            uint64_t bal[4];  // ballots of pk, taken where pk is computed (SGPR results, no 0/1 VGPRs)
             if (AID_K2_COLDSKIP && !(hcur[s % kRowsPerStep] & wmask)) {
                 // every key the wave's windows see is 0: fm = 0, no candidate (p = 0 is never > the
                 // threshold); only the vertical ring advances and row r-7 is decided
@@ -275,6 +281,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                     const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
                     m7p[i] = m7;
                     pk[i] = pend[(s + 1) & 7][i] >= m7;
+                    bal[i] = __ballot(pk[i]);
                     pend[s][i] = -1;
                 }
             } else {
@@ -349,14 +356,15 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
                 const int bf = max(max(i == 0 ? max(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
                 m7p[i] = m7;
-                // candidate: p > before (strict) and p >= right window; keys >= 0, so -1 = none
-                const int c1 = (p > bf) ? p : -1;
                 // row r-7 (slot s+1) has now met all 7 later rows: p >= their row-max
                 pk[i] = pend[(s + 1) & 7][i] >= m7;
-                pend[s][i] = (c1 >= R[i]) ? c1 : -1;
+                bal[i] = __ballot(pk[i]);
+                // candidate: p > before (strict) and p >= right window, i.e. p >= max(before + 1, right)
+                // (integer keys <= 0x7F800000: no overflow); keys >= 0, so -1 = none
+                pend[s][i] = (p >= max(bf + 1, R[i])) ? p : -1;
             }
             }
-            const uint64_t b0 = __ballot(pk[0]), b1 = __ballot(pk[1]), b2 = __ballot(pk[2]), b3 = __ballot(pk[3]);
+            const uint64_t b0 = bal[0], b1 = bal[1], b2 = bal[2], b3 = bal[3];
             const int rd = r - kPeakDT;
 #if AID_K2_BRANCHFREE
             {
