@@ -58,6 +58,9 @@ constexpr int kRowsPerStep = 4;
 #define AID_K2_BRANCHFREE 0  // measured slower (K2 0.1709 -> 0.1789 ms: zero-row loads cost more than the branch). 1: row loads of cold blocks read a zero row and the mask store of other lanes/rows
                              // goes to a dummy sink (per-lane address selects) instead of exec-masked branches
 #endif
+#ifndef AID_K2_MSTORE
+#define AID_K2_MSTORE 0  // mask-word store: 0 = lane-indexed select, 1 = v_writelane, 2 = lane 0 stores 32 B
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
 #endif
@@ -71,6 +74,12 @@ constexpr int kRowsPerStep = 4;
 #ifndef AID_K2_FMAXKEY
 #define AID_K2_FMAXKEY 1  // K2 0.1709 -> 0.1623 ms same-box (r02). 1: the key is the bits of v_max_f32(0, x) (maxNum: a NaN gives 0, +-0 gives +0)
 #endif
+template <int LANE>
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t s_val) {  // v[LANE] = s_val (uniform)
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s_val), "i"(LANE));
+    return v;
+}
+
 __device__ __forceinline__ int pkey(float x) {
 #if AID_K2_FMAXKEY
     // one VALU instead of v_cmp + v_cndmask (+ the VCC hazard's s_nop). Same keys: the plane holds K1's
@@ -373,9 +382,32 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 *dstw = wv;
             }
 #else
-            if (rd >= t0 && rd < t1 && lane < 4) {
-                const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-                M[(int64_t)rd * kMaskWords] = wv;
+            if (rd >= t0 && rd < t1) {
+#if AID_K2_MSTORE == 1
+                // lane i < 4 stores ballot word i: 8 v_writelane of the SGPR ballots
+                uint32_t lo = 0, hi = 0;
+                lo = write_lane<0>(lo, (uint32_t)b0);
+                hi = write_lane<0>(hi, (uint32_t)(b0 >> 32));
+                lo = write_lane<1>(lo, (uint32_t)b1);
+                hi = write_lane<1>(hi, (uint32_t)(b1 >> 32));
+                lo = write_lane<2>(lo, (uint32_t)b2);
+                hi = write_lane<2>(hi, (uint32_t)(b2 >> 32));
+                lo = write_lane<3>(lo, (uint32_t)b3);
+                hi = write_lane<3>(hi, (uint32_t)(b3 >> 32));
+                if (lane < 4) M[(int64_t)rd * kMaskWords] = ((uint64_t)hi << 32) | lo;
+#elif AID_K2_MSTORE == 2
+                // the wave's 4 words are contiguous (word 4 wave + i): lane 0 stores all 32 bytes
+                if (lane == 0) {
+                    uint4 *d = reinterpret_cast<uint4 *>(M + (int64_t)rd * kMaskWords);
+                    d[0] = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+                    d[1] = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+                }
+#else
+                if (lane < 4) {
+                    const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+                    M[(int64_t)rd * kMaskWords] = wv;
+                }
+#endif
             }
 #endif
         }
