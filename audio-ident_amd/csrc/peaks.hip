@@ -136,8 +136,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     const int t1 = min(t0 + strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
-#if AID_K2_BRANCHFREE
+#if AID_K2_BRANCHFREE || AID_K2_MSTORE == 3
     uint64_t *sinkw = sink + (int64_t)(blockIdx.x & (kK2SinkBlocks - 1)) * 256 + threadIdx.x;  // other stores
+    (void)zero_row;
 #else
     (void)sink;
     (void)zero_row;
@@ -380,6 +381,15 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
                 uint64_t *dstw = (rd >= t0 && rd < t1 && lane < 4) ? M + (int64_t)rd * kMaskWords : sinkw;
                 *dstw = wv;
+            }
+#elif AID_K2_MSTORE == 3
+            {
+                // one mask store per row on every path (a row outside the strip goes to the sink): the
+                // store count between a row fetch and its use is then the same on every path, so the
+                // wait before staging is vmcnt(4) instead of a vmcnt(0) that also waited for the stores
+                const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+                uint64_t *dstw = (rd >= t0 && rd < t1) ? M + (int64_t)rd * kMaskWords : sinkw;
+                if (lane < 4) *dstw = wv;
             }
 #else
             if (rd >= t0 && rd < t1) {

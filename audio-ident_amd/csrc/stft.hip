@@ -82,6 +82,26 @@
 #ifndef AID_K1_BRANCHFREE
 #define AID_K1_BRANCHFREE 1  // K1 0.2935 -> 0.2863 ms same-box (r02)
 #endif
+// AID_K1_TPF_W / _A / _B: table prefetch. hipcc issued every window / twiddle ds_read_b128 right before
+// its use behind its own s_waitcnt lgkmcnt(0) (24 serialized LDS round trips per frame). With these set,
+// the first N float4 reads of the window (W), the stage-A twiddles (A, before stage A's DFT16) and the
+// stage-B twiddles (B, before stage B's DFT16) are issued together ahead of a sched_barrier, the rest
+// right after the DFT16.
+#ifndef AID_K1_TPF_W
+#define AID_K1_TPF_W 8  // K1 0.2804 -> 0.2778 ms same-box (r02; 0.2752 with AID_K1_PREWAIT)
+#endif
+#ifndef AID_K1_TPF_A
+#define AID_K1_TPF_A 0
+#endif
+#ifndef AID_K1_TPF_B
+#define AID_K1_TPF_B 0
+#endif
+#ifndef AID_K1_TPF_S  // 1: the real split's 24 LDS reads (E3 pairs + split twiddles) issued up front
+#define AID_K1_TPF_S 0
+#endif
+#ifndef AID_K1_PREWAIT
+#define AID_K1_PREWAIT 1  // K1 0.2804 -> 0.2785 ms alone, 0.2752 with AID_K1_TPF_W (same-box, r02)
+#endif
 // AID_K1_COMPACT=1: E1/E2 through unpadded 1024-entry buffers with XOR column swizzles
 // (8 KB per wave instead of 8.5 KB), so 16 waves + tables fit in 160 KB of LDS
 
@@ -292,6 +312,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     float2 ring[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) ring[r] = src[64 * r];
+#if AID_K1_PREWAIT
+    // the segment's first frame needs the whole ring anyway: wait for it here, so the frame loop's
+    // header does not inherit this path's pending loads (hipcc's wait at the header, merged over both
+    // edges, was vmcnt(1): every 4 frames the wave also waited for the previous frame's 17 stores)
+    // (an empty asm reading every ring register: hipcc must complete the loads before it)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(ring[r].x), "v"(ring[r].y));
+#endif
 #if AID_K1_WINREG
     float4 wreg[8];
 #pragma unroll
@@ -304,10 +332,18 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
             const int f = f0 + p;
             if (f < nfr) {  // wave-uniform
                 float2 v[16];
+#if AID_K1_TPF_W
+                float4 wpf[8];
+#pragma unroll
+                for (int h = 0; h < AID_K1_TPF_W; ++h) wpf[h] = s_win4[64 * h + lane];
+                __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
                 for (int h = 0; h < 8; ++h) {
 #if AID_K1_WINREG
                     const float4 w = wreg[h];
+#elif AID_K1_TPF_W
+                    const float4 w = h < AID_K1_TPF_W ? wpf[h] : s_win4[64 * h + lane];
 #else
                     const float4 w = s_win4[64 * h + lane];
 #endif
@@ -324,11 +360,25 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         ring[(ROWS * p + j) & 15] = src[(int64_t)fn * HOP2 + 64 * (16 - ROWS + j)];
                 }
                 // stage A: lane = n2
+#if AID_K1_TPF_A
+                float4 tpa[8];
+#pragma unroll
+                for (int h = 0; h < AID_K1_TPF_A; ++h) tpa[h] = s_ta4[64 * h + lane];
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 if (AID_K1_DIAG != 9) dft16(v, t16);
+#if AID_K1_TPF_A
+#pragma unroll
+                for (int h = AID_K1_TPF_A; h < 8; ++h) tpa[h] = s_ta4[64 * h + lane];
+#endif
                 // T1K[n2*k1]; lane 0 multiplies by T1K[0] = (1,-0): value-identical (FPSPEC 4 note)
 #pragma unroll
                 for (int h = 0; h < 8; ++h) {
+#if AID_K1_TPF_A
+                    const float4 t = tpa[h];
+#else
                     const float4 t = s_ta4[64 * h + lane];
+#endif
                     if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
                     v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
                 }
@@ -368,10 +418,24 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #if AID_K1_PRIO
                 __builtin_amdgcn_s_setprio(0);
 #endif
+#if AID_K1_TPF_B
+                float4 tpb[8];
+#pragma unroll
+                for (int h = 0; h < AID_K1_TPF_B; ++h) tpb[h] = s_tb4[4 * h + mq];
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 if (AID_K1_DIAG != 9) dft16(v, t16);
+#if AID_K1_TPF_B
+#pragma unroll
+                for (int h = AID_K1_TPF_B; h < 8; ++h) tpb[h] = s_tb4[4 * h + mq];
+#endif
 #pragma unroll
                 for (int h = 0; h < 8; ++h) {
+#if AID_K1_TPF_B
+                    const float4 t = tpb[h];
+#else
                     const float4 t = s_tb4[4 * h + mq];
+#endif
                     if (h) v[2 * h] = cmul(v[2 * h], make_float2(t.x, t.y));
                     v[2 * h + 1] = cmul(v[2 * h + 1], make_float2(t.z, t.w));
                 }
@@ -475,15 +539,34 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     // workgroup's dummy row (a scalar select: no branch splits the arithmetic)
                     uint32_t hotw = 0;
                     float po[8], pm[8];
+#if AID_K1_TPF_S
+                    // every read of the split issued up front (v is dead here: its 32 VGPRs hold them)
+                    float2 sa[8], sb[8], st[8];
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
+                        sa[i] = buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
+                        sb[i] = buf[(i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i)];
+                        st[i] = s_t2[64 * i + lane];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+#if AID_K1_TPF_S
+                        const float2 a = sa[i], bs = sb[i];
+#else
                         const float2 a = buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
                         const int bi = (i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
                         const float2 bs = buf[bi];
+#endif
                         const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
                         const float er = a.x + b.x, ei = a.y - b.y;
                         const float orr = a.y + b.y, oi = b.x - a.x;
+#if AID_K1_TPF_S
+                        const float2 t2h = st[i];
+#else
                         const float2 t2h = s_t2[64 * i + lane];
+#endif
                         const float2 tw = cmul(make_float2(orr, oi), make_float2(t2h.x, t2h.y));
                         const float xr = er + tw.x, xi = ei + tw.y;
                         po[i] = __builtin_fmaf(xr, xr, xi * xi);  // Q = 4P (see below)
