@@ -59,7 +59,10 @@ constexpr int kRowsPerStep = 4;
                              // goes to a dummy sink (per-lane address selects) instead of exec-masked branches
 #endif
 #ifndef AID_K2_MSTORE
-#define AID_K2_MSTORE 0  // mask-word store: 0 = lane-indexed select, 1 = v_writelane, 2 = lane 0 stores 32 B
+#define AID_K2_MSTORE 1  // mask-word store: 0 = lane-indexed select (hipcc lowered it to a switch of exec-masked
+                         // blocks, ~14 instructions per row), 1 = v_writelane of the SGPR ballots (K2 0.1515 ->
+                         // 0.1427 ms same-box, r02), 2 = lane 0 stores 32 B, 3 = store on every path (2/3: 130
+                         // VGPRs, occupancy 3)
 #endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
