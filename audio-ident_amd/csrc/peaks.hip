@@ -64,8 +64,13 @@ constexpr int kRowsPerStep = 4;
                          // 0.1427 ms same-box, r02), 2 = lane 0 stores 32 B, 3 = store on every path (2/3: 130
                          // VGPRs, occupancy 3)
 #endif
+#ifndef AID_K2_WCOLD
+#define AID_K2_WCOLD 1  // 1: a wave whose window blocks are cold in every row of the strip skips the row loop
+                        // (K2 0.1418 -> 0.1302-0.1350 ms same-box, r02; needs AID_K2_MIN_WAVES 4: 130 VGPRs
+                        // otherwise, occupancy 3)
+#endif
 #ifndef AID_K2_MIN_WAVES
-#define AID_K2_MIN_WAVES 1  // 4 caps VGPRs at 128 (occupancy 4) at the cost of scratch spills
+#define AID_K2_MIN_WAVES 4  // 4 caps VGPRs at 128 (occupancy 4; no spills since r02: 122 VGPRs with AID_K2_WCOLD)
 #endif
 
 // Peak decisions compare powers as int32 keys: a power is >= +0 (never -0: FPSPEC 4's
@@ -197,6 +202,36 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 #else
     auto hotword = [&](int r) -> uint32_t { return (r >= 0 && r < F) ? HW[r] : 0u; };
 #endif
+    // blocks 4w-1 .. 4w+4 hold the wave's bins and their +-15 neighbours
+    const uint32_t wmask = (0x3Fu << (4 * wave)) >> 1;
+#if AID_K2_WCOLD
+    {
+        // strip-cold wave: if those blocks are cold in every row the strip reads, every key this wave
+        // stages or compares is 0, so it has no candidate and its mask words are 0 (exact, as the
+        // per-row cold skip). It writes those zeros, zeroes its staged bins once (the neighbouring
+        // waves' windows read them), and only keeps the workgroup's barrier count (2 per 4 rows)
+        uint32_t acc = 0;
+        for (int r = rbeg + lane; r < rbeg + iters; r += 64) acc |= (r >= 0 && r < F) ? HW[r] : 0u;
+        if (__ballot((acc & wmask) != 0u) == 0) {
+#pragma unroll
+            for (int b = 0; b < AID_K2_NBUF; ++b)
+#pragma unroll
+                for (int j = 0; j < kRowsPerStep; ++j) {
+                    reinterpret_cast<int4 *>(&rows[b][j][16])[tid] = make_int4(0, 0, 0, 0);
+#if AID_K2_BLOCKMAX
+                    bms[b][j][4 + tid] = 0;
+#endif
+                }
+            uint64_t *Mz = mask + fb * kMaskWords + 4 * wave + (lane & 3);
+            for (int r = t0 + (lane >> 2); r < t1; r += 16) Mz[(int64_t)r * kMaskWords] = 0;
+            for (int it = 0; it < iters; it += kRowsPerStep) {
+                if (AID_K2_NBUF == 1 && it > 0) __syncthreads();
+                __syncthreads();
+            }
+            return;
+        }
+    }
+#endif
     float4 pf[AID_K2_PF];  // rows of the next batch(es), in flight
 #pragma unroll
     for (int j = 0; j < AID_K2_PF; ++j) {
@@ -217,8 +252,6 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     uint32_t hsave[kRowsPerStep], hcur[kRowsPerStep];
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) hsave[j] = hcur[j] = hotword(rbeg + j);
-    // blocks 4w-1 .. 4w+4 hold the wave's bins and their +-15 neighbours
-    const uint32_t wmask = (0x3Fu << (4 * wave)) >> 1;
 
     for (int base = 0; base < iters; base += 8) {
 #pragma unroll
