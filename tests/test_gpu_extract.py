@@ -226,3 +226,30 @@ def test_profile_select_masks_kernels(gpu_engine):
         gpu_engine.profile_enable(False)
         gpu_engine.profile_select(None)
         gpu_engine.profile_read(reset=True)
+
+
+def test_band_limited_quarters_bit_exact(gpu_engine):
+    """Content confined to one or two bands, with tones on the 64-bin block and 256-bin quarter
+    edges: K2's per-wave strip-cold skip (a quarter whose +-1-block window is cold in every row of
+    the strip writes zero mask words without running the row loop) is taken by different waves in
+    different clips, and the hot quarters' +-15-bin windows straddle the skipped ones."""
+    rng = np.random.default_rng(5)
+    n = 44100 * 3
+    t = np.arange(n) / SR
+    clips = []
+    for bins in ([10], [250, 262], [511, 513], [700], [767, 769, 1000], [60, 1010], [383, 384, 449]):
+        x = np.zeros(n)
+        for k in bins:
+            f = k * SR / 2048.0
+            am = 0.5 + 0.5 * np.sin(2 * np.pi * rng.uniform(1, 4) * t + rng.uniform(0, 6))
+            x += 0.05 * am * np.sin(2 * np.pi * f * t + rng.uniform(0, 6))
+        x += rng.standard_normal(n) * 1e-4
+        clips.append(np.clip(x, -1, 1).astype(np.float32))
+    got = gpu_engine.extract_host(clips)
+    for c, x in enumerate(clips):
+        ref_pk = O.peaks(O.stft_power(x, HOP))
+        pk = peaks_from_mask(gpu_engine.peakmask(c, len(x)))
+        assert np.array_equal(pk, ref_pk.reshape(-1, 2)), f"clip {c}: peaks differ"
+        ref = O.fingerprint(x, HOP)
+        assert len(ref) > 0
+        assert np.array_equal(got[c], ref), f"clip {c}: hashes differ"
