@@ -99,6 +99,12 @@
 #ifndef AID_K1_TPF_S  // 1: the real split's 24 LDS reads (E3 pairs + split twiddles) issued up front
 #define AID_K1_TPF_S 0
 #endif
+#ifndef AID_K1_HOTSUP
+#define AID_K1_HOTSUP 1  // 1: a mirror ballot marks blocks 15-i and 16-i together (superset hot word)
+#endif
+#ifndef AID_K1_STBR
+#define AID_K1_STBR 1  // 1: cold-block stores skipped by scalar branches instead of redirected to a sink row
+#endif
 #ifndef AID_K1_PREWAIT
 #define AID_K1_PREWAIT 1  // K1 0.2804 -> 0.2785 ms alone, 0.2752 with AID_K1_TPF_W (same-box, r02)
 #endif
@@ -577,8 +583,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         hotw |= __ballot(po[i] > thr) ? 1u << i : 0u;  // bins 64i..64i+63
                         // lanes 1..63: bins of block 15 - i; lane 0 (i > 0): block 16 - i
                         const uint64_t hb = __ballot(pm[i] > thr);
+#if AID_K1_HOTSUP
+                        // one test marks both blocks: a superset of the hot blocks (exact for K2, which
+                        // only skips blocks marked cold), 3 scalar ops instead of 6 + a 64-bit VALU compare
+                        hotw |= hb ? (i == 0 ? 1u << 15 : 3u << (15 - i)) : 0u;
+#else
                         hotw |= (hb >> 1) ? 1u << (15 - i) : 0u;
                         hotw |= (hb & 1) ? 1u << (16 - i) : 0u;
+#endif
                     }
                     {  // bin 512 pairs with itself: every lane computes it (same address, same value),
                        // so its store and the hot word's need no lane-0 branch
@@ -593,6 +605,18 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     hotw = __builtin_amdgcn_readfirstlane(hotw);
                     dhot[f] = hotw;
                     const uint32_t hsel = keep ? 0x1FFFFu : hotw;  // one select, not a branch per store
+#if AID_K1_STBR
+                    // cold stores skipped by scalar branches (the powers are all computed above, so the
+                    // branches no longer split the arithmetic)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if ((hsel >> i) & 1u) drow[lane + 64 * i] = po[i];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t need = (hsel >> (15 - i)) | (i > 0 ? hsel >> (16 - i) : 0u);
+                        if ((need & 1u) && (i > 0 || lane != 0)) drow[1024 - (lane + 64 * i)] = pm[i];
+                    }
+#else
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         float *b = ((hsel >> i) & 1u) ? drow : dummy;
@@ -608,6 +632,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         if (i == 0) b = lane == 0 ? dummy : b;  // lane 0's mirror of k = 0 is not a bin
                         b[1024 - (lane + 64 * i)] = pm[i];
                     }
+#endif
                 } else
 #endif
                 {
