@@ -587,6 +587,13 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
                              e->mask.p, e->k2_zero.p, e->k2_sink.p, s);
         }
+#ifdef AID_K2_TWICE  // diagnostic: a second K2 over the same rows (cache state after the first)
+        {
+            ProfScope ps(e, AID_K_PEAKS, s, true);
+            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
+                             e->mask.p, e->k2_zero.p, e->k2_sink.p, s);
+        }
+#endif
         if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,

@@ -113,6 +113,20 @@
 
 namespace aid {
 
+// power-row store: AID_K1_NTSTORE=1 marks it non-temporal (streaming): K1 0.268 -> 0.266 ms, K2 0.134 ->
+// 0.130 ms, 5.88 -> 5.95 M audio-s/s same-box (r02). A second K2 over the same rows right after the first
+// (AID_K2_TWICE diagnostic) takes as long as the first, so K2 is not bound by draining K1's dirty lines
+#ifndef AID_K1_NTSTORE
+#define AID_K1_NTSTORE 1
+#endif
+__device__ __forceinline__ void pstore(float *p, float v) {
+#if AID_K1_NTSTORE
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // E3 slot of Z[k]: XOR-swizzle bits 2-3 by bits 4-5. The stage-C writers of one 16-lane
 // group hold k = kq + 16*mq (+const): k ^ (mq << 2) puts them on 16 distinct 8-byte bank
 // pairs; the readers (k = lane + 64i, and the mirror 1024-k) stay a permutation of one or two
@@ -313,6 +327,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + lane;
     float *dst = out + (clips[lo].frame_base + t0) * kBins;
     float *dummy = dummy_rows + (int64_t)(blockIdx.x & (kK1DummyRows - 1)) * 2048;  // cold-block store sink
+    (void)dummy;  // unused with AID_K1_STBR
     uint32_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
 
     float2 ring[16];
@@ -599,7 +614,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float2 tw = cmul(make_float2(orr, oi), t512);
                         const float xr = er + tw.x, xi = ei + tw.y;
                         const float p512 = __builtin_fmaf(xr, xr, xi * xi);
-                        drow[512] = p512;
+                        pstore(drow + 512, p512);
                         hotw |= p512 > thr ? 1u << 8 : 0u;
                     }
                     hotw = __builtin_amdgcn_readfirstlane(hotw);
@@ -610,11 +625,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     // branches no longer split the arithmetic)
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
-                        if ((hsel >> i) & 1u) drow[lane + 64 * i] = po[i];
+                        if ((hsel >> i) & 1u) pstore(drow + lane + 64 * i, po[i]);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         const uint32_t need = (hsel >> (15 - i)) | (i > 0 ? hsel >> (16 - i) : 0u);
-                        if ((need & 1u) && (i > 0 || lane != 0)) drow[1024 - (lane + 64 * i)] = pm[i];
+                        if ((need & 1u) && (i > 0 || lane != 0)) pstore(drow + 1024 - (lane + 64 * i), pm[i]);
                     }
 #else
 #pragma unroll
