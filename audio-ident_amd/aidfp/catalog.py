@@ -99,7 +99,10 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     t0 = time.perf_counter()
     pcm = torch.empty(max(1, min(batch, len(mine))) * n, dtype=torch.float32, device="cuda")
     base = eng.index_stats()["postings"]
-    s = torch.cuda.current_stream()
+    # one non-default stream for generation, extraction and the posting append: events recorded on
+    # the legacy default stream would serialise against the engine's (blocking) stream every batch
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
     ev = []
     for b0 in range(0, len(mine), batch):
         tr = mine[b0 : b0 + batch]
@@ -108,7 +111,7 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
         eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
         b.record(s)
         ev.append((a, b))
-        eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n)
+        eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n, s.cuda_stream)
         eng.index_add_extracted(tr)
     del pcm
     torch.cuda.synchronize()

@@ -20,8 +20,8 @@ LIB = PKG / "aidfp" / "libaidfp.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "stream.hip", "resample.hip",
-           "dedup.hip", "exact.hip", "engine.cpp"]
+SOURCES = ["stft.hip", "peaks.hip", "landmarks.hip", "synth.hip", "index.hip", "index_sort.hip", "stream.hip",
+           "resample.hip", "dedup.hip", "exact.hip", "engine.cpp"]
 FLAGS = [
     f"--offload-arch={ARCH}",
     "-O3",

@@ -46,6 +46,11 @@ void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, c
 void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                           const uint8_t *tomb, uint32_t n_tracks, uint32_t *cursor, uint64_t *post, hipStream_t s);
 void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
+size_t index_sort_temp_bytes(int64_t n);
+hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
+                                   const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
+                                   uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes,
+                                   uint32_t *cnt, uint64_t **vals_out, hipStream_t s);
 void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
                     uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
                     uint32_t *ot, hipStream_t s);
@@ -149,6 +154,10 @@ struct aid_engine {
     uint32_t n_tracks = 0;        // max track id + 1
     DevBuf<uint32_t> idx_cnt, idx_off, scan_tmp;
     DevBuf<uint64_t> idx_post;
+    DevBuf<uint32_t> srt_k0, srt_k1;  // K4 sort build: key double buffer
+    DevBuf<uint64_t> srt_v;           // K4 sort build: the value buffer idx_post pairs with
+    DevBuf<uint8_t> srt_tmp;          // K4 sort build: radix-sort temporary storage
+    int k4_mode = 1;                  // AIDFP_K4: 1 = sort build (default), 0 = atomic counting sort
     bool index_built = false, index_dirty = true;
     int64_t n_indexed = 0;
     int64_t n_buckets_used = 0;
@@ -337,6 +346,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
         e->k5_parts = v >= 4 ? 4 : v >= 2 ? 2 : v >= 1 ? 1 : 0;
     }
     if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
+    if (const char *k4 = std::getenv("AIDFP_K4")) e->k4_mode = std::strcmp(k4, "atomic") == 0 ? 0 : 1;
     if (const char *kp = std::getenv("AIDFP_K5_PATH"))
         e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
     // blocking stream: ordered against the legacy default stream (torch's default), so device
@@ -401,6 +411,10 @@ void aid_engine_destroy(aid_engine *e) {
     e->idx_off.release();
     e->scan_tmp.release();
     e->idx_post.release();
+    e->srt_k0.release();
+    e->srt_k1.release();
+    e->srt_v.release();
+    e->srt_tmp.release();
     e->nz.release();
     e->q_recs.release();
     e->q_start.release();
@@ -1185,14 +1199,32 @@ static int finalize_locked(aid_engine *e) {
     HIP_TRY(e->idx_post.reserve((size_t)std::max<int64_t>(e->n_post, 1)));
     if (e->n_tracks == 0) HIP_TRY(e->tomb.reserve(1024));
     HIP_TRY(hipMemsetAsync(e->idx_cnt.p, 0, K * sizeof(uint32_t), s));
-    launch_index_count(e->p_hash.p, e->p_track.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p, s);
     HIP_TRY(e->nz.reserve(1));
     HIP_TRY(hipMemsetAsync(e->nz.p, 0, sizeof(unsigned long long), s));
-    launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
-    launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
-    HIP_TRY(hipMemcpyAsync(e->idx_cnt.p, e->idx_off.p, K * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    launch_index_scatter(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p,
-                         e->idx_post.p, s);
+    if (e->k4_mode == 1 && e->n_post > 0) {
+        // sort build (index_sort.hip): keys + values -> stable radix sort -> bucket lengths -> scan
+        const size_t np = (size_t)e->n_post;
+        const size_t tb = index_sort_temp_bytes(e->n_post);
+        if (tb == 0) return fail(AID_ERR_DEVICE, "radix sort: temporary storage query failed");
+        HIP_TRY(e->srt_k0.reserve(np));
+        HIP_TRY(e->srt_k1.reserve(np));
+        HIP_TRY(e->srt_v.reserve(np));
+        HIP_TRY(e->srt_tmp.reserve(tb));
+        uint64_t *sorted = nullptr;
+        HIP_TRY(launch_index_sort_build(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks,
+                                        e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
+                                        e->idx_cnt.p, &sorted, s));
+        if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended
+        launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
+        launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
+    } else {
+        launch_index_count(e->p_hash.p, e->p_track.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p, s);
+        launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
+        launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
+        HIP_TRY(hipMemcpyAsync(e->idx_cnt.p, e->idx_off.p, K * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        launch_index_scatter(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p,
+                             e->idx_post.p, s);
+    }
     HIP_TRY(hipGetLastError());
     uint32_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, e->idx_off.p + (K - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));

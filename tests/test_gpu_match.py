@@ -191,3 +191,37 @@ def test_zero_hash_track_has_a_slot():
         eng.index_remove(77)
         with pytest.raises(Exception):
             eng.index_remove(77)
+
+
+def test_sort_build_equals_atomic_build(monkeypatch):
+    """K4 sort build (index_sort.hip, default) vs the atomic counting sort (AIDFP_K4=atomic): same live
+    postings and identical query rows, with removed tracks (sentinel keys sorted past the live ones)."""
+    import torch
+
+    n = SR * 12
+    tracks = np.arange(20, dtype=np.uint32) * 7 + 3
+    rng = np.random.default_rng(5)
+    qs = [synth.synth(int(tracks[i]), int(rng.integers(0, 7 * SR)), 5 * SR, SR, snr_db=20.0, salt=40 + i)
+          for i in range(0, 20, 2)]
+    out = {}
+    for mode in ("atomic", "sort"):
+        monkeypatch.setenv("AIDFP_K4", mode)
+        eng = Engine(SR)
+        try:
+            pcm = torch.empty(len(tracks) * n, dtype=torch.float32, device="cuda")
+            eng.synth(pcm.data_ptr(), tracks, np.zeros(len(tracks), np.int64), n)
+            eng.extract_device(pcm.data_ptr(), np.arange(len(tracks) + 1, dtype=np.int64) * n)
+            eng.index_add_extracted(tracks)
+            eng.index_remove(int(tracks[4]))
+            eng.index_remove(int(tracks[10]))
+            eng.index_finalize()
+            recs = [O.fingerprint(q, HOP) for q in qs]
+            out[mode] = (eng.index_stats(), eng.query(recs))
+        finally:
+            eng.close()
+    (sa, ra), (ss, rs) = out["atomic"], out["sort"]
+    assert sa["live"] == ss["live"] > 0 and sa["postings"] == ss["postings"]
+    assert any(len(r) for r in rs)
+    for q, (a, b) in enumerate(zip(ra, rs)):
+        assert np.array_equal(a, b), f"query {q}: rows differ between the builds"
+        assert not np.isin(b[:, 1] if len(b) else [], [tracks[4], tracks[10]]).any()
