@@ -190,6 +190,8 @@ struct aid_engine {
     DevBuf<uint32_t> x_tracks;
     size_t hist_zero_cap = 0;  // q_hist capacity known to be all-zero
 
+    int64_t *h_stage = nullptr;  // pinned staging of aid_index_add_extracted
+    size_t h_stage_cap = 0;
     ClipDesc *h_desc = nullptr;  // pinned
     size_t h_desc_cap = 0;
     // extraction call hazards, tracked with events instead of a stream sync per call:
@@ -451,6 +453,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->g_recv.release();
     e->x_tracks.release();
     if (e->h_desc) (void)hipHostFree(e->h_desc);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->desc_ev) (void)hipEventDestroy(e->desc_ev);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
     if (e->d_tab) (void)hipFree(e->d_tab);
@@ -1065,13 +1068,26 @@ int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids) {
     hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
     const int n = e->n_clips;
     if (n == 0) return AID_OK;
-    std::vector<int64_t> counts(n), dst(n);
-    HIP_TRY(hipMemcpyAsync(counts.data(), e->counts.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    // pinned staging [counts n][src n][dst n][tracks n/2+1] (int64 slots): the H2D copies below run
+    // asynchronously; the next call's counts sync orders its rewrite of the staging after them
+    const size_t need = 3 * (size_t)n + (size_t)n / 2 + 1;
+    if (need > e->h_stage_cap) {
+        if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
+        e->h_stage = nullptr;
+        e->h_stage_cap = 0;
+        HIP_TRY(hipHostMalloc((void **)&e->h_stage, need * sizeof(int64_t)));
+        e->h_stage_cap = need;
+    }
+    int64_t *counts = e->h_stage, *src = counts + n, *dst = src + n;
+    uint32_t *trk = reinterpret_cast<uint32_t *>(dst + n);
+    HIP_TRY(hipMemcpyAsync(counts, e->counts.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     int64_t tot = 0;
     uint32_t mx = 0;
     for (int c = 0; c < n; ++c) {
+        src[c] = e->clip_base[c];
         dst[c] = e->n_post + tot;
+        trk[c] = track_ids[c];
         tot += counts[c];
         mx = std::max(mx, track_ids[c] + 1);
     }
@@ -1080,13 +1096,12 @@ int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids) {
     HIP_TRY(e->x_src.reserve(n));
     HIP_TRY(e->x_dst.reserve(n));
     HIP_TRY(e->x_tracks.reserve(n));
-    HIP_TRY(hipMemcpyAsync(e->x_src.p, e->clip_base.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(e->x_dst.p, dst.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(e->x_tracks.p, track_ids, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_src.p, src, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_dst.p, dst, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->x_tracks.p, trk, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     launch_records_to_postings(e->records.p, e->x_src.p, e->counts.p, e->x_dst.p, e->x_tracks.p, n, e->p_hash.p,
                                e->p_track.p, e->p_t.p, s);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipGetLastError());  // no sync: every reader of the posting planes syncs last_stream first
     e->n_post += tot;
     e->index_dirty = true;
     return AID_OK;
@@ -1364,6 +1379,8 @@ int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t
     if (count == 0) return AID_OK;
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
+    // the posting append of aid_index_add_extracted runs asynchronously on the caller's stream
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     const hipMemcpyKind k = location == AID_PCM_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     HIP_TRY(hipMemcpy(hash, e->p_hash.p + first, count * sizeof(uint32_t), k));
     HIP_TRY(hipMemcpy(track, e->p_track.p + first, count * sizeof(uint32_t), k));

@@ -32,6 +32,16 @@ constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
                         // (K3 0.0341 -> 0.0268 ms same-box, r02)
 #endif
 
+#ifndef AID_K3_DIRECT
+#define AID_K3_DIRECT 1  // one chunk per clip: the workgroup's clip is its chunk index (no binary search)
+#endif
+#ifndef AID_K3_COALESCED
+#define AID_K3_COALESCED 0  // 1: phase 1 reads the mask words coalesced (16 lanes per frame): measured slower (K3 0.0265 -> 0.037 ms; the per-thread runs issue all 32 loads at once)
+#endif
+#ifndef AID_K3_ONEWALK
+#define AID_K3_ONEWALK 1  // the write pass reuses the count walk's accepted targets (first anchor per thread)
+#endif
+
 #ifndef AID_K3_WSCAN
 #define AID_K3_WSCAN 1  // 1: wave scans (shuffles) + one LDS exchange of wave totals: 2 barriers per scan, not 20
 #endif
@@ -110,6 +120,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     const int64_t chunk = blockIdx.x;
     if (chunk >= total_chunks) return;
     int lo = 0, hi = n_clips - 1;
+    if (AID_K3_DIRECT && total_chunks == n_clips) lo = (int)chunk;  // one chunk per clip: no search
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (clips[mid].chunk_base <= chunk) lo = mid; else hi = mid - 1;
@@ -129,6 +140,20 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     const int per = (nf + kK3 - 1) / kK3;
     const int fa = min(tid * per, nf), fz = min(fa + per, nf);
     int64_t mine = 0;
+#if AID_K3_COALESCED
+    // counts read coalesced: 16 consecutive lanes take the 16 mask words of one frame (a wave reads 512
+    // contiguous bytes per load; the per-thread frame runs read 64 scattered 8-B words per load)
+    for (int e = tid; e < nf * kMaskWords; e += kK3) {
+        uint32_t c = (uint32_t)__popcll(Mc[e]);
+        c += __shfl_xor(c, 8, 16);
+        c += __shfl_xor(c, 4, 16);
+        c += __shfl_xor(c, 2, 16);
+        c += __shfl_xor(c, 1, 16);
+        if ((e & (kMaskWords - 1)) == 0) foff[e / kMaskWords] = c;
+    }
+    __syncthreads();
+    for (int f = fa; f < fz; ++f) mine += foff[f];
+#else
     for (int f = fa; f < fz; ++f) {
         uint32_t c = 0;
 #pragma unroll
@@ -136,6 +161,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
         foff[f] = c;
         mine += c;
     }
+#endif
     int64_t npk = 0;
     int64_t run = block_excl_scan(mine, scan_tmp, &npk);
     // 2. expand to the (t,k)-ordered peak list (unshuffling K2's ballot layout)
@@ -179,10 +205,16 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     const int pa_per = (n_anchor + kK3 - 1) / kK3;
     const int aa = min(tid * pa_per, n_anchor), az = min(aa + pa_per, n_anchor);
     int64_t my = 0;
+    // the thread's first anchor keeps its accepted targets as a bitmask of walk positions j - i - 1 < 64
+    // (AID_K3_ONEWALK), so the write pass emits them without walking the zone again
+    uint64_t tmask = 0;
+    bool tmask_ok = false;
     for (int i = aa; i < az; ++i) {
         const uint32_t a = plist[i];
         const int ta = (int)(a >> 10), ka = (int)(a & 1023);
         int got = 0;
+        uint64_t mk = 0;
+        bool ok = true;
         for (int j = i + 1; j < (int)npk && got < kFan; ++j) {
             const uint32_t b = plist[j];
             const int dt = (int)(b >> 10) - ta;
@@ -190,7 +222,15 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
             if (dt <= 0) continue;
             const int df = (int)(b & 1023) - ka;
             if (df < -kZoneDF || df > kZoneDF) continue;
+            if (AID_K3_ONEWALK) {
+                if (j - i - 1 < 64) mk |= 1ull << (j - i - 1);
+                else ok = false;
+            }
             ++got;
+        }
+        if (AID_K3_ONEWALK && i == aa) {
+            tmask = mk;
+            tmask_ok = ok;
         }
         my += got;
     }
@@ -221,6 +261,13 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
             const uint32_t a = plist[i];
             const int ta = (int)(a >> 10), ka = (int)(a & 1023);
             const uint64_t t1 = (uint64_t)(c0 + ta) << 32;
+            if (AID_K3_ONEWALK && i == aa && tmask_ok) {
+                for (uint64_t m = tmask; m; m &= m - 1) {
+                    const uint32_t b = plist[i + 1 + (__ffsll((unsigned long long)m) - 1)];
+                    out[o++] = t1 | make_hash(ka, (int)(b & 1023), (int)(b >> 10) - ta);
+                }
+                continue;
+            }
             int got = 0;
             for (int j = i + 1; j < (int)npk && got < kFan; ++j) {
                 const uint32_t b = plist[j];
