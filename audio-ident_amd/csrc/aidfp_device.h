@@ -43,6 +43,25 @@ __device__ __forceinline__ float2 cmul(float2 x, float2 w) {
     return make_float2(__builtin_fmaf(x.x, w.x, -(x.y * w.y)), __builtin_fmaf(x.x, w.y, x.y * w.x));
 }
 
+// FPSPEC cmul by the three DFT16 twiddles whose binary32 table values are structured (checked on the host
+// in aid_engine_create: T16[2] = (c, -c), T16[6] = (-c, -c), T16[4] = (e, -1)). Each returns exactly
+// cmul(x, w): x.im * w.im is -(x.im * c) (or x.im * e, -x.im) bit for bit, so one product serves both
+// components -- 3 VALU instead of 4.
+#ifndef AID_DFT16_SYM
+#define AID_DFT16_SYM 1
+#endif
+__device__ __forceinline__ float2 cmul_w2(float2 x, float c) {  // w = (c, -c)
+    const float t = x.y * c;  // -(x.im * w.im) and x.im * w.re
+    return make_float2(__builtin_fmaf(x.x, c, t), __builtin_fmaf(x.x, -c, t));
+}
+__device__ __forceinline__ float2 cmul_w6(float2 x, float mc) {  // w = (mc, mc), mc = -c
+    const float t = x.y * mc;  // x.im * w.im = x.im * w.re
+    return make_float2(__builtin_fmaf(x.x, mc, -t), __builtin_fmaf(x.x, mc, t));
+}
+__device__ __forceinline__ float2 cmul_w4(float2 x, float e) {  // w = (e, -1): -(x.im * -1) = x.im
+    return make_float2(__builtin_fmaf(x.x, e, x.y), __builtin_fmaf(x.x, -1.0f, x.y * e));
+}
+
 // FPSPEC 3 DFT4, in place on (a,b,c,d) -> (y0,y1,y2,y3)
 __device__ __forceinline__ void dft4(float2 &a, float2 &b, float2 &c, float2 &d) {
     float2 t0 = cadd(a, c), t1 = csub(a, c), t2 = cadd(b, d), t3 = csub(b, d);
@@ -60,14 +79,22 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10]) 
     for (int b = 0; b < 4; ++b) dft4(v[b], v[b + 4], v[b + 8], v[b + 12]);
     // twiddles W16^{b*c}, b,c in 1..3
     v[1 + 4 * 1] = cmul(v[1 + 4 * 1], t16[1]);
-    v[1 + 4 * 2] = cmul(v[1 + 4 * 2], t16[2]);
     v[1 + 4 * 3] = cmul(v[1 + 4 * 3], t16[3]);
+    v[3 + 4 * 1] = cmul(v[3 + 4 * 1], t16[3]);
+    v[3 + 4 * 3] = cmul(v[3 + 4 * 3], t16[9]);
+#if AID_DFT16_SYM
+    v[1 + 4 * 2] = cmul_w2(v[1 + 4 * 2], t16[2].x);
+    v[2 + 4 * 1] = cmul_w2(v[2 + 4 * 1], t16[2].x);
+    v[2 + 4 * 2] = cmul_w4(v[2 + 4 * 2], t16[4].x);
+    v[2 + 4 * 3] = cmul_w6(v[2 + 4 * 3], t16[6].x);
+    v[3 + 4 * 2] = cmul_w6(v[3 + 4 * 2], t16[6].x);
+#else
+    v[1 + 4 * 2] = cmul(v[1 + 4 * 2], t16[2]);
     v[2 + 4 * 1] = cmul(v[2 + 4 * 1], t16[2]);
     v[2 + 4 * 2] = cmul(v[2 + 4 * 2], t16[4]);
     v[2 + 4 * 3] = cmul(v[2 + 4 * 3], t16[6]);
-    v[3 + 4 * 1] = cmul(v[3 + 4 * 1], t16[3]);
     v[3 + 4 * 2] = cmul(v[3 + 4 * 2], t16[6]);
-    v[3 + 4 * 3] = cmul(v[3 + 4 * 3], t16[9]);
+#endif
     // second DFT4 over b for each c: inputs v[0+4c..3+4c], outputs out[c + 4d]
     float2 o[16];
 #pragma unroll

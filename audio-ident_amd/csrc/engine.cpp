@@ -368,6 +368,16 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
             delete e;
             return fail(AID_ERR_DEVICE, "twiddle table lacks the mirror symmetry K1 relies on");
         }
+    // K1's DFT16 (AID_DFT16_SYM, aidfp_device.h) shares one product in the cmuls by T16[2], T16[4], T16[6]
+    {
+        const float2 w2 = h->t16[2], w4 = h->t16[4], w6 = h->t16[6];
+        if (!(w2.y == -w2.x && w6.x == w6.y && w6.x == -w2.x && w4.y == -1.0f)) {
+            delete h;
+            (void)hipStreamDestroy(e->own_stream);
+            delete e;
+            return fail(AID_ERR_DEVICE, "DFT16 twiddle table lacks the symmetry K1 relies on");
+        }
+    }
     std::vector<int16_t> sin_tab(4096);
     for (int k = 0; k < 4096; ++k) sin_tab[k] = (int16_t)nearbyint(32767.0 * sin(2.0 * M_PI * (double)k / 4096.0));
     he = hipMalloc(&e->d_tab, sizeof(Tables));

@@ -105,6 +105,9 @@
 #ifndef AID_K1_STBR
 #define AID_K1_STBR 1  // 1: cold-block stores skipped by scalar branches instead of redirected to a sink row
 #endif
+#ifndef AID_K1_MIRROR_ID
+#define AID_K1_MIRROR_ID 1  // real split: the mirror bin reuses the direct bin's twiddle product (see there)
+#endif
 #ifndef AID_K1_PREWAIT
 #define AID_K1_PREWAIT 1  // K1 0.2804 -> 0.2785 ms alone, 0.2752 with AID_K1_TPF_W (same-box, r02)
 #endif
@@ -591,8 +594,15 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float2 tw = cmul(make_float2(orr, oi), make_float2(t2h.x, t2h.y));
                         const float xr = er + tw.x, xi = ei + tw.y;
                         po[i] = __builtin_fmaf(xr, xr, xi * xi);  // Q = 4P (see below)
+#if AID_K1_MIRROR_ID
+                        // the mirror bin's product cmul((orr, -oi), (-t2.re, t2.im)) is (-tw.x, tw.y) bit for bit:
+                        // its re is fma(orr, -c, oi*s) = -fma(orr, c, -(oi*s)) (round-to-nearest is odd-symmetric)
+                        // and its im is fma(orr, s, (-oi)*(-c)) = tw.y; so xr2 = er + (-tw.x), xi2 = -ei + tw.y
+                        const float xr2 = er - tw.x, xi2 = tw.y - ei;
+#else
                         const float2 tw2 = cmul(make_float2(orr, -oi), make_float2(-t2h.x, t2h.y));
                         const float xr2 = er + tw2.x, xi2 = -ei + tw2.y;
+#endif
                         // k = 0 (lane 0, i = 0): the mirror is the dropped Nyquist bin
                         pm[i] = (i == 0 && lane == 0) ? 0.f : __builtin_fmaf(xr2, xr2, xi2 * xi2);
                         hotw |= __ballot(po[i] > thr) ? 1u << i : 0u;  // bins 64i..64i+63
