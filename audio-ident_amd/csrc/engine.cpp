@@ -343,6 +343,8 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
+    if (const char *kx = std::getenv("AIDFP_K2_SLOTS_X"))  // K2 strips per resident workgroup slot (experiment)
+        e->k2_slots = std::max<int64_t>(1, (int64_t)(e->k2_slots * std::max(0.25, std::atof(kx))));
     if (const char *kp = std::getenv("AIDFP_K5_PARTS")) {  // 1, 2 or 4 (0 = by vote count)
         const int v = std::atoi(kp);
         e->k5_parts = v >= 4 ? 4 : v >= 2 ? 2 : v >= 1 ? 1 : 0;

@@ -69,6 +69,9 @@ constexpr int kRowsPerStep = 4;
                         // (K2 0.1418 -> 0.1302-0.1350 ms same-box, r02; needs AID_K2_MIN_WAVES 4: 130 VGPRs
                         // otherwise, occupancy 3)
 #endif
+#ifndef AID_K2_WCOLD_EXIT
+#define AID_K2_WCOLD_EXIT 0  // 1: a strip-cold wave exits after zeroing its LDS bins and mask words
+#endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 4  // 4 caps VGPRs at 128 (occupancy 4; no spills since r02: 122 VGPRs with AID_K2_WCOLD)
 #endif
@@ -224,11 +227,19 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 }
             uint64_t *Mz = mask + fb * kMaskWords + 4 * wave + (lane & 3);
             for (int r = t0 + (lane >> 2); r < t1; r += 16) Mz[(int64_t)r * kMaskWords] = 0;
+#if AID_K2_WCOLD_EXIT
+            // the wave terminates: s_barrier waits only for a workgroup's surviving waves, and its
+            // registers go to waves of workgroups still waiting for a slot (host: AIDFP_K2_SLOTS_X); its
+            // zeroed LDS bins are written before it ends
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            return;
+#else
             for (int it = 0; it < iters; it += kRowsPerStep) {
                 if (AID_K2_NBUF == 1 && it > 0) __syncthreads();
                 __syncthreads();
             }
             return;
+#endif
         }
     }
 #endif
