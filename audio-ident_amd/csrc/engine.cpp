@@ -27,9 +27,12 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
                        uint32_t *hot, float thr, bool keep_power, float *dummy, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
-                      const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink, hipStream_t s);
+                      const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink, uint32_t *cold_cnt,
+                      hipStream_t s);
+bool peak_pick_counts_cold();
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
-                      int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s);
+                      int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
+                      uint64_t *k2_cold_host, uint32_t k2_waves, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
                   int noise_a, uint32_t salt, const int16_t *sin_tab, hipStream_t s);
 int64_t resample_lds_floats(int up, int down, int J);
@@ -139,6 +142,10 @@ struct aid_engine {
     DevBuf<float> k1_dummy;  // K1's sink for cold-block stores: kK1DummyRows x 2048 floats
     DevBuf<float> k2_zero;   // K2: a 1024-float zero row (cold-block loads)
     DevBuf<uint64_t> k2_sink;  // K2: mask-store sink, kK2SinkBlocks x 256 words
+    DevBuf<uint32_t> k2_cold;  // K2: strip-cold wave counters (64), summed and reset by K3
+    uint64_t *h_cold = nullptr;      // pinned, host-mapped: K3 stores (cold waves | waves << 32) of the last K2 here
+    uint64_t *h_cold_dev = nullptr;  // its device address
+    double k2_slots_x = 0.0;         // AIDFP_K2_SLOTS_X: fixed strips per slot; 0 = adaptive (extract_locked)
     DevBuf<ClipDesc> desc;
     DevBuf<int64_t> chunk_counts;
     DevBuf<uint64_t> records;
@@ -343,8 +350,8 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
-    if (const char *kx = std::getenv("AIDFP_K2_SLOTS_X"))  // K2 strips per resident workgroup slot (experiment)
-        e->k2_slots = std::max<int64_t>(1, (int64_t)(e->k2_slots * std::max(0.25, std::atof(kx))));
+    if (const char *kx = std::getenv("AIDFP_K2_SLOTS_X"))  // fixed K2 strips per slot (0 = adaptive, the default)
+        e->k2_slots_x = std::max(0.0, std::atof(kx));
     if (const char *kp = std::getenv("AIDFP_K5_PARTS")) {  // 1, 2 or 4 (0 = by vote count)
         const int v = std::atoi(kp);
         e->k5_parts = v >= 4 ? 4 : v >= 2 ? 2 : v >= 1 ? 1 : 0;
@@ -410,6 +417,8 @@ void aid_engine_destroy(aid_engine *e) {
     e->k1_dummy.release();
     e->k2_zero.release();
     e->k2_sink.release();
+    e->k2_cold.release();
+    if (e->h_cold) (void)hipHostFree(e->h_cold);
     e->mask.release();
     e->desc.release();
     e->chunk_counts.release();
@@ -515,7 +524,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     // a different stream than the previous call's: order against it the simple way
     if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
     // same offsets and PCM location as the descriptors already on the device: no re-upload
-    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() == (size_t)n_clips + 2 &&
+    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() == (size_t)n_clips + 3 &&
                      e->desc_key[n_clips + 1] == loc;
     for (int c = 0; desc_same && c <= n_clips; ++c) desc_same = e->desc_key[c] == offsets[c];
     // h_desc is rewritten below: the previous descriptor upload must have left it
@@ -528,7 +537,22 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     int64_t frames = 0, strips = 0, chunks = 0, recs = 0, staged = 0, kstrips = 0;
     bool empty_clip = false;  // a clip without frames gets no count from K3: zero the counts first
     for (int c = 0; c < n_clips; ++c) e->clip_frames[c] = num_frames(offsets[c + 1] - offsets[c], hop);
-    const int strip_len = peak_strip_len(e->clip_frames.data(), n_clips, e->k2_slots);
+    // K2 strips per resident workgroup slot. Strip-cold K2 waves exit (peaks.hip AID_K2_WCOLD_EXIT) and their
+    // registers admit more workgroups per CU (LDS allows 7 instead of the 4 of an all-hot CU): with the
+    // fraction c of cold waves counted in earlier calls (K3 stores it in pinned memory; read without a sync,
+    // so it lags a few calls), the strips are made shorter and more numerous, 0.75 / (1 - c) per slot,
+    // quantised to 1, 1.25, 1.5 (a stable key for the cached descriptors)
+    double kx = e->k2_slots_x;
+    if (kx <= 0.0) {
+        kx = 1.0;
+        const uint64_t cw = e->h_cold ? *reinterpret_cast<volatile uint64_t *>(e->h_cold) : 0;
+        if (cw >> 32) {
+            const double c = std::min(1.0, (double)(uint32_t)cw / (double)(cw >> 32));
+            kx = c >= 0.45 ? 1.5 : c >= 0.3 ? 1.25 : 1.0;
+        }
+    }
+    const int strip_len = peak_strip_len(e->clip_frames.data(), n_clips, std::max<int64_t>(1, (int64_t)(e->k2_slots * kx)));
+    desc_same = desc_same && e->desc_key[n_clips + 2] == strip_len;  // strip bases depend on the strip length
     for (int c = 0; c < n_clips; ++c) {
         const int64_t n = offsets[c + 1] - offsets[c];
         const int64_t F = num_frames(n, hop);
@@ -566,6 +590,15 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         HIP_TRY(hipMemsetAsync(e->k2_zero.p, 0, kBins * sizeof(float), s));
     }
     HIP_TRY(e->k2_sink.reserve((size_t)kK2SinkBlocks * 256));
+    if (!e->k2_cold.p) {
+        HIP_TRY(e->k2_cold.reserve(64));
+        HIP_TRY(hipMemsetAsync(e->k2_cold.p, 0, 64 * sizeof(uint32_t), s));
+    }
+    if (!e->h_cold && peak_pick_counts_cold()) {
+        HIP_TRY(hipHostMalloc((void **)&e->h_cold, sizeof(uint64_t), hipHostMallocMapped));
+        *e->h_cold = 0;
+        HIP_TRY(hipHostGetDevicePointer((void **)&e->h_cold_dev, e->h_cold, 0));
+    }
     HIP_TRY(e->chunk_counts.reserve((size_t)chunks + 1));
     HIP_TRY(e->records.reserve((size_t)recs + 1));
     HIP_TRY(e->counts.reserve((size_t)n_clips + 1));
@@ -591,6 +624,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         e->desc_ev_live = true;
         e->desc_key.assign(offsets, offsets + n_clips + 1);
         e->desc_key.push_back(loc);
+        e->desc_key.push_back(strip_len);
         e->desc_dev_for_key = e->desc.p;
     }
     if (empty_clip || frames == 0) HIP_TRY(hipMemsetAsync(e->counts.p, 0, sizeof(int64_t) * ((size_t)n_clips + 1), s));
@@ -614,24 +648,24 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         {
             ProfScope ps(e, AID_K_PEAKS, s, true);
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
-                             e->mask.p, e->k2_zero.p, e->k2_sink.p, s);
+                             e->mask.p, e->k2_zero.p, e->k2_sink.p, e->k2_cold.p, s);
         }
 #ifdef AID_K2_TWICE  // diagnostic: a second K2 over the same rows (cache state after the first)
         {
             ProfScope ps(e, AID_K_PEAKS, s, true);
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
-                             e->mask.p, e->k2_zero.p, e->k2_sink.p, s);
+                             e->mask.p, e->k2_zero.p, e->k2_sink.p, e->k2_cold.p, s);
         }
 #endif
         if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
-                             false, s);
+                             false, nullptr, nullptr, 0u, s);
         }
         {
             ProfScope ps(e, AID_K_LANDMARK_WRITE, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
-                             true, s);
+                             true, e->h_cold_dev ? e->k2_cold.p : nullptr, e->h_cold_dev, (uint32_t)(4 * strips), s);
         }
     }
     HIP_TRY(hipGetLastError());

@@ -112,12 +112,23 @@ __device__ __forceinline__ uint32_t make_hash(int k1, int k2, int dt) {
 template <bool WRITE>
 __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ mask, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_chunks, int64_t *__restrict__ chunk_counts,
-                                                  uint64_t *__restrict__ records, int64_t *__restrict__ clip_counts) {
+                                                  uint64_t *__restrict__ records, int64_t *__restrict__ clip_counts,
+                                                  uint32_t *__restrict__ k2_cold, uint64_t *__restrict__ k2_cold_host,
+                                                  uint32_t k2_waves) {
     __shared__ uint32_t plist[kHashChunkPeakCap];
     __shared__ uint32_t foff[kHashChunk + kZoneDT + 2];
     __shared__ int64_t scan_tmp[kK3];
     const int tid = threadIdx.x;
     const int64_t chunk = blockIdx.x;
+    if (WRITE && k2_cold && blockIdx.x == 0 && tid < 64) {
+        // K2's strip-cold wave count (peaks.hip) and the wave count of that same launch, stored together as
+        // one 8-byte word in host-mapped memory for the next call's strip sizing (no sync: a stale pair only
+        // delays the adaptation), then the counters are reset for the next K2
+        uint32_t c = k2_cold[tid];
+        k2_cold[tid] = 0u;
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if (tid == 0) *reinterpret_cast<volatile uint64_t *>(k2_cold_host) = (uint64_t)c | ((uint64_t)k2_waves << 32);
+    }
     if (chunk >= total_chunks) return;
     int lo = 0, hi = n_clips - 1;
     if (AID_K3_DIRECT && total_chunks == n_clips) lo = (int)chunk;  // one chunk per clip: no search
@@ -285,14 +296,15 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
 }
 
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
-                      int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, hipStream_t s) {
+                      int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
+                      uint64_t *k2_cold_host, uint32_t k2_waves, hipStream_t s) {
     if (total_chunks <= 0) return;
     if (write)
         timed_launch(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
-                           total_chunks, chunk_counts, records, clip_counts);
+                           total_chunks, chunk_counts, records, clip_counts, k2_cold, k2_cold_host, k2_waves);
     else
         timed_launch(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
-                           total_chunks, chunk_counts, records, clip_counts);
+                           total_chunks, chunk_counts, records, clip_counts, (uint32_t *)nullptr, (uint64_t *)nullptr, 0u);
 }
 
 }  // namespace aid

@@ -70,7 +70,7 @@ constexpr int kRowsPerStep = 4;
                         // otherwise, occupancy 3)
 #endif
 #ifndef AID_K2_WCOLD_EXIT
-#define AID_K2_WCOLD_EXIT 0  // 1: a strip-cold wave exits after zeroing its LDS bins and mask words
+#define AID_K2_WCOLD_EXIT 1  // 1: a strip-cold wave exits after zeroing its LDS bins and mask words
 #endif
 #ifndef AID_K2_MIN_WAVES
 #define AID_K2_MIN_WAVES 4  // 4 caps VGPRs at 128 (occupancy 4; no spills since r02: 122 VGPRs with AID_K2_WCOLD)
@@ -107,7 +107,8 @@ __device__ __forceinline__ int pkey(float x) {
 __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
                                                   const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask,
-                                                  const float4 *__restrict__ zero_row, uint64_t *__restrict__ sink) {
+                                                  const float4 *__restrict__ zero_row, uint64_t *__restrict__ sink,
+                                                  uint32_t *__restrict__ cold_cnt) {
     __shared__ __attribute__((aligned(16))) int rows[AID_K2_NBUF][kRowsPerStep][kBins + 32];
 #if AID_K2_BLOCKMAX
     __shared__ __attribute__((aligned(16))) int bms[AID_K2_NBUF][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
@@ -230,7 +231,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 #if AID_K2_WCOLD_EXIT
             // the wave terminates: s_barrier waits only for a workgroup's surviving waves, and its
             // registers go to waves of workgroups still waiting for a slot (host: AIDFP_K2_SLOTS_X); its
-            // zeroed LDS bins are written before it ends
+            // zeroed LDS bins are written before it ends. The cold waves are counted (64 counters, read
+            // and reset by K3) so the host can size the next call's strips (extract_locked)
+            if (lane == 0 && cold_cnt) atomicAdd(&cold_cnt[blockIdx.x & 63], 1u);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             return;
 #else
@@ -473,11 +476,12 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
 
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
                       float thr, const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink,
-                      hipStream_t s) {
+                      uint32_t *cold_cnt, hipStream_t s) {
     if (total_strips <= 0) return;
     timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
-                       strip_len, thr, hot, mask, reinterpret_cast<const float4 *>(zero_row), sink);
+                       strip_len, thr, hot, mask, reinterpret_cast<const float4 *>(zero_row), sink, cold_cnt);
 }
+bool peak_pick_counts_cold() { return AID_K2_WCOLD && AID_K2_WCOLD_EXIT; }
 
 // resident K2 workgroups per CU (registers / LDS), for sizing strips to one round
 int peak_pick_blocks_per_cu() {
