@@ -196,6 +196,10 @@ def main() -> int:
         "traffic_source": pmc_src,
         "duration_source": kern[dom]["pass"],
         "extraction_kernels_ms_per_step": round(sum(v["ms_per_launch"] for v in kern.values() if v["ms_per_launch"]), 4),
+        # the whole step against the same staged-dataflow accounting (K1 + K2 bytes of SURVEY 8(d); K3's
+        # mask reads and record writes are < 1 % and left out): how far the pipeline is from streaming
+        "step_staged_bytes": alg["stft_power"] + alg["peak_pick"],
+        "step_achieved": round((alg["stft_power"] + alg["peak_pick"]) / (elapsed / args.steps) / 1e9, 1),
         "note": "achieved = SURVEY 8(d) staged-dataflow bytes (PCM + the full power plane); K1 stores only hot "
                 "64-bin blocks and K2 reads only those, so the PMC traffic can be below the algorithmic bytes",
     }
