@@ -11,3 +11,4 @@ bash profiles/run_rocprof.sh $TAG > gpurun_out/full_prof.log 2>&1
 timeout -k 10 300 python bench_match.py > gpurun_out/full_match.json 2> gpurun_out/full_match.err
 timeout -k 10 300 python bench_stream.py > gpurun_out/full_stream48.json 2> gpurun_out/full_stream48.err
 timeout -k 10 300 python bench_stream.py --index-sr 16000 > gpurun_out/full_stream16.json 2> gpurun_out/full_stream16.err
+timeout -k 10 300 python bench_catalog.py > gpurun_out/full_catalog.json 2> gpurun_out/full_catalog.err
