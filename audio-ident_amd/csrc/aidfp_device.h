@@ -71,12 +71,59 @@ __device__ __forceinline__ void dft4(float2 &a, float2 &b, float2 &c, float2 &d)
     d = make_float2(t1.x - t3.y, t1.y + t3.x);
 }
 
+// AID_PK_DFT4=1: the DFT4 butterflies as packed FP32 (v_pk_add_f32 on (re, im) register pairs; the -i
+// rotations through op_sel/neg modifiers). Same IEEE binary32 additions as dft4() above, bit for bit:
+// 8 VALU instead of 16 per DFT4 (a packed add issues at ~1.1-1.2x the pair rate of two scalar adds,
+// probes/pk_add_probe: so the gain is issue slots and ~10 % of the butterflies' VALU time).
+#ifndef AID_PK_DFT4
+#define AID_PK_DFT4 0
+#endif
+typedef float aid_pk2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ aid_pk2 pk_of(float2 a) { return (aid_pk2){a.x, a.y}; }
+__device__ __forceinline__ float2 f2_of(aid_pk2 a) { return make_float2(a.x, a.y); }
+__device__ __forceinline__ aid_pk2 pk_add(aid_pk2 a, aid_pk2 b) {
+    aid_pk2 r;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ aid_pk2 pk_sub(aid_pk2 a, aid_pk2 b) {
+    aid_pk2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ aid_pk2 pk_add_mi(aid_pk2 a, aid_pk2 b) {  // (a.re + b.im, a.im - b.re)
+    aid_pk2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ aid_pk2 pk_add_pi(aid_pk2 a, aid_pk2 b) {  // (a.re - b.im, a.im + b.re)
+    aid_pk2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ aid_pk2 pk_mul(aid_pk2 a, aid_pk2 b) {
+    aid_pk2 r;
+    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ void dft4_pk(float2 &a, float2 &b, float2 &c, float2 &d) {
+    const aid_pk2 x0 = pk_of(a), x1 = pk_of(b), x2 = pk_of(c), x3 = pk_of(d);
+    const aid_pk2 t0 = pk_add(x0, x2), t1 = pk_sub(x0, x2), t2 = pk_add(x1, x3), t3 = pk_sub(x1, x3);
+    a = f2_of(pk_add(t0, t2));
+    c = f2_of(pk_sub(t0, t2));
+    b = f2_of(pk_add_mi(t1, t3));
+    d = f2_of(pk_add_pi(t1, t3));
+}
+
 // FPSPEC 3 DFT16: v[16] in natural input order -> out[c + 4d] in v (natural output order).
 // t16 holds W16^1, W16^2, W16^3, W16^4 (unused), W16^6, W16^9 at indices 1,2,3,4,6,9.
 __device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10]) {
     // s[b][c] lives in v[b + 4c] after the first DFT4 over (b, b+4, b+8, b+12)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) dft4(v[b], v[b + 4], v[b + 8], v[b + 12]);
+    for (int b = 0; b < 4; ++b) {
+        if (AID_PK_DFT4) dft4_pk(v[b], v[b + 4], v[b + 8], v[b + 12]);
+        else dft4(v[b], v[b + 4], v[b + 8], v[b + 12]);
+    }
     // twiddles W16^{b*c}, b,c in 1..3
     v[1 + 4 * 1] = cmul(v[1 + 4 * 1], t16[1]);
     v[1 + 4 * 3] = cmul(v[1 + 4 * 3], t16[3]);
@@ -100,7 +147,8 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10]) 
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         float2 a0 = v[0 + 4 * c], a1 = v[1 + 4 * c], a2 = v[2 + 4 * c], a3 = v[3 + 4 * c];
-        dft4(a0, a1, a2, a3);
+        if (AID_PK_DFT4) dft4_pk(a0, a1, a2, a3);
+        else dft4(a0, a1, a2, a3);
         o[c + 0] = a0;
         o[c + 4] = a1;
         o[c + 8] = a2;

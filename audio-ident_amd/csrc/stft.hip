@@ -105,6 +105,9 @@
 #ifndef AID_K1_STBR
 #define AID_K1_STBR 1  // 1: cold-block stores skipped by scalar branches instead of redirected to a sink row
 #endif
+#ifndef AID_K1_PK_WIN
+#define AID_K1_PK_WIN 0  // 1: window multiply as 16 v_pk_mul_f32 per frame instead of 32 v_mul_f32
+#endif
 #ifndef AID_K1_MIRROR_ID
 #define AID_K1_MIRROR_ID 1  // real split: the mirror bin reuses the direct bin's twiddle product (see there)
 #endif
@@ -372,8 +375,13 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     const float4 w = s_win4[64 * h + lane];
 #endif
                     const float2 x0 = ring[(2 * h + ROWS * p) & 15], x1 = ring[(2 * h + 1 + ROWS * p) & 15];
+#if AID_K1_PK_WIN
+                    v[2 * h] = f2_of(pk_mul(pk_of(x0), (aid_pk2){w.x, w.y}));
+                    v[2 * h + 1] = f2_of(pk_mul(pk_of(x1), (aid_pk2){w.z, w.w}));
+#else
                     v[2 * h] = make_float2(x0.x * w.x, x0.y * w.y);
                     v[2 * h + 1] = make_float2(x1.x * w.z, x1.y * w.w);
+#endif
                 }
                 // the rows just consumed (n1 < ROWS) are replaced by frame f+1's new rows (after the
                 // last frame of the segment: a harmless re-load of its own rows, instead of a branch)
