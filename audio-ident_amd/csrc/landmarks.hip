@@ -32,6 +32,12 @@ constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
                         // (K3 0.0341 -> 0.0268 ms same-box, r02)
 #endif
 
+#ifndef AID_K3_DIAG
+#define AID_K3_DIAG 0  // timing-only ablations (wrong results): 1 = stop after the counts, 2 = after the peak list
+#endif
+#ifndef AID_K3_SPARSE
+#define AID_K3_SPARSE 1  // expand peaks from the OR of each 256-bin block's ballot words (no unshuffle)
+#endif
 #ifndef AID_K3_DIRECT
 #define AID_K3_DIRECT 1  // one chunk per clip: the workgroup's clip is its chunk index (no binary search)
 #endif
@@ -175,6 +181,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
 #endif
     int64_t npk = 0;
     int64_t run = block_excl_scan(mine, scan_tmp, &npk);
+    if (AID_K3_DIAG == 1) return;  // timing only: phase 1 (counts + scan)
     // 2. expand to the (t,k)-ordered peak list (unshuffling K2's ballot layout)
     for (int f = fa; f < fz; ++f) {
         const uint32_t c = foff[f];
@@ -188,6 +195,20 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
         uint64_t W[kMaskWords];
 #pragma unroll
         for (int w = 0; w < kMaskWords; ++w) W[w] = Mc[f * kMaskWords + w];
+#if AID_K3_SPARSE
+        // no unshuffle: a 4-bin group holds at most one peak (FPSPEC 5: no two peaks within +-15 bins), so the
+        // OR of a 256-bin block's 4 ballot words has one bit per peak, in ascending bin order; the word
+        // holding that bit gives the bin's offset i in the group (bin = 256 b + 4 l + i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t w1 = W[4 * b + 1], w2 = W[4 * b + 2], w3 = W[4 * b + 3];
+            for (uint64_t m = W[4 * b] | w1 | w2 | w3; m; m &= m - 1) {
+                const int l = __ffsll((unsigned long long)m) - 1;
+                const int i = (int)((w1 >> l) & 1) + 2 * (int)((w2 >> l) & 1) + 3 * (int)((w3 >> l) & 1);
+                plist[idx++] = ((uint32_t)f << 10) | (uint32_t)(256 * b + 4 * l + i);
+            }
+        }
+#else
 #if AID_K3_SKIP0
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -206,10 +227,12 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
                 }
             }
         }
+#endif
         run += c;
     }
     if (tid == 0) foff[nf] = (uint32_t)npk;
     __syncthreads();
+    if (AID_K3_DIAG == 2) return;  // timing only: phases 1-2 (peak list built)
     const int n_anchor = (int)foff[c1 - c0];
 
     // 3. anchors: contiguous run per thread
