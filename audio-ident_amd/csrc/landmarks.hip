@@ -33,7 +33,8 @@ constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
 #endif
 
 #ifndef AID_K3_DIAG
-#define AID_K3_DIAG 0  // timing-only ablations (wrong results): 1 = stop after the counts, 2 = after the peak list
+#define AID_K3_DIAG 0  // timing-only ablations (wrong results): 1 = stop after the counts, 2 = after the peak list,
+                       // 3 = after the pair counts
 #endif
 #ifndef AID_K3_SPARSE
 #define AID_K3_SPARSE 1  // expand peaks from the OR of each 256-bin block's ballot words (no unshuffle)
@@ -270,6 +271,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     }
     int64_t chunk_total = 0;
     const int64_t excl = block_excl_scan(my, scan_tmp, &chunk_total);
+    if (AID_K3_DIAG == 3) return;  // timing only: phases 1-3 (pair counts + scan, no records)
     if constexpr (!WRITE) {
         if (tid == 0) chunk_counts[chunk] = chunk_total;
     } else {
