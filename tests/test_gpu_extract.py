@@ -253,3 +253,21 @@ def test_band_limited_quarters_bit_exact(gpu_engine):
         ref = O.fingerprint(x, HOP)
         assert len(ref) > 0
         assert np.array_equal(got[c], ref), f"clip {c}: hashes differ"
+
+
+@pytest.mark.parametrize("slots_x", ["1", "1.25", "1.5", "3"])
+def test_k2_strip_multipliers_bit_exact(monkeypatch, slots_x):
+    """K2's strip count follows the measured cold-wave fraction (1, 1.25 or 1.5 strips per resident
+    workgroup slot, engine.cpp extract_locked; strip-cold waves exit). Every fixed multiplier, including
+    one that leaves workgroups waiting for slots, gives the oracle's peaks and hashes bit for bit, on a
+    band-limited batch where about half of the quarter waves are strip-cold and exit."""
+    from aidfp.engine import Engine
+
+    monkeypatch.setenv("AIDFP_K2_SLOTS_X", slots_x)
+    clips = [_clip(t, 44100 * 4 + 313 * t, snr=None if t % 3 else 20) for t in range(24)]
+    with Engine(SR) as eng:
+        got = eng.extract_host(clips)
+        for c, x in enumerate(clips):
+            pk = peaks_from_mask(eng.peakmask(c, len(x)))
+            assert np.array_equal(pk, O.peaks(O.stft_power(x, HOP)).reshape(-1, 2)), f"clip {c}: peaks differ"
+            assert np.array_equal(got[c], O.fingerprint(x, HOP)), f"clip {c}: hashes differ"
