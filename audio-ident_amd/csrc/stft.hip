@@ -271,6 +271,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     const int e3a0 = lane, e3a1 = lane ^ 8;
     const int e3b1 = (64 - lane) ^ 12, e3b0 = (64 - lane) ^ 4;
     const int e3b4 = (lane == 0) ? 76 : e3b0;  // i = 4: Z[768] for lane 0
+#define AID_E3A(i) ((i) < 4 ? e3a0 : e3a1)
+#define AID_E3B(i) ((i) < 4 ? e3b1 : (i) == 4 ? e3b4 : e3b0)
     const float s1 = mq < 2 ? 1.0f : -1.0f;                     // butterfly over lanes (mq, mq ^ 2)
     const float s2 = (mq == 1 || mq == 2) ? -1.0f : 1.0f;       // butterfly over lanes (mq, mq ^ 1)
     const float s0 = lane == 0 ? 1.0f : -1.0f;  // sign of Z[0]'s mirror slot for i = 0 (Z[0] itself)
@@ -587,8 +589,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #if AID_K1_TPF_S
                         const float2 a = sa[i], bs = sb[i];
 #else
-                        const float2 a = buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
-                        const int bi = (i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
+                        const float2 a = buf[AID_E3A(i) + 64 * i];
+                        const int bi = (i == 0 && lane == 0) ? 0 : AID_E3B(i) + 64 * (15 - i);
                         const float2 bs = buf[bi];
 #endif
                         const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
