@@ -21,6 +21,10 @@ constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 #endif
 constexpr int kStftWaves = AID_STFT_WAVES;
 constexpr int kStftStrip = 16;
+#ifndef AID_K1_MIN_FRAMES
+#define AID_K1_MIN_FRAMES 2  // frames per K1 wave when the batch has fewer than 16 per resident wave
+#endif
+constexpr int kK1MinFrames = AID_K1_MIN_FRAMES;
 constexpr int kK1DummyRows = 256;
 constexpr int kK2SinkBlocks = 1024;  // K2 mask-store sinks: 256 u64 per workgroup index mod 1024 (2 MB)  // K1 cold-block store sinks (one 8 KB row per workgroup index mod 256)
 #ifndef AID_K1_COMPACT
@@ -30,7 +34,8 @@ constexpr int kStftLdsPerWave = AID_K1_COMPACT ? 1024 : 1088;  // float2 entries
 
 // K2: output frames per workgroup strip, sized per call (peak_strip_len) between these bounds
 #ifndef AID_PEAK_STRIP_MIN
-#define AID_PEAK_STRIP_MIN 64  // shorter strips re-read too much halo (14 rows per strip)
+#define AID_PEAK_STRIP_MIN 16  // shorter strips re-read more halo (14 rows per strip); only batches with fewer
+                               // than ~64 frames per resident K2 slot get them (a streaming window: 465 frames)
 #endif
 constexpr int kPeakStripMin = AID_PEAK_STRIP_MIN;
 

@@ -803,8 +803,11 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
                        uint32_t *hot, float thr, bool keep_power, float *dummy, hipStream_t s) {
     if (total_frames <= 0) return;
 #if AID_K1_BALANCED
-    // one round of equal ranges; at least kStftStrip frames per wave (a ring fill per segment)
-    const int64_t n_waves = std::max<int64_t>(1, std::min<int64_t>(slots, total_frames / kStftStrip));
+    // one round of equal ranges. A wave reloads its 16-row ring once per segment, so large batches keep
+    // >= kStftStrip frames per wave; a batch smaller than that spreads over >= kK1MinFrames-frame ranges
+    // instead (a 5 s window, 465 frames: 29 waves x 16 frames ran 77 us of serial frames per wave)
+    const int64_t n_waves = std::max<int64_t>(
+        1, total_frames >= slots * kStftStrip ? slots : std::min<int64_t>(slots, total_frames / kK1MinFrames));
     const int64_t total = total_frames;
 #else
     const int64_t n_waves = total_strips, total = total_strips;
