@@ -1538,6 +1538,8 @@ int aid_index_load(aid_engine *e, const char *path) {
 #ifndef AID_K5_PER_BUCKET
 #define AID_K5_PER_BUCKET 2.0  // forwarded votes (1-bit filter estimate) per global histogram bucket
 #endif
+constexpr int kSpeculateQueries = 16;  // run_queries: LDS match path launched with the vote counts
+
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
                        int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
     const int mr = e->cfg.max_results;
@@ -1554,7 +1556,34 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(h_votes.data(), e->q_votes.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     }
+    // a few queries (a stream window, one upload's sub-windows): run the LDS path right away in the same
+    // round trip as the vote counts instead of after them (one host sync less per call). It is exact at
+    // any load (an overflowing query reports -1 and falls through to the global path below); only its
+    // speed suffers for heavy queries, which a handful of them bounds
+    const bool speculate = e->k5_path == 0 && nq <= kSpeculateQueries;
+    std::vector<int32_t> spec_n;
+    if (speculate) {
+        {
+            ProfScope ps(e, AID_K_MATCH, s);
+            launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, s);
+        }
+        HIP_TRY(hipGetLastError());
+        spec_n.resize(nq);
+        if (rows)
+            HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(spec_n.data(), e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
+    if (speculate) {
+        std::vector<int> again;
+        for (int q = 0; q < nq; ++q) {
+            if (spec_n[q] < 0) again.push_back(q);
+            else nrows[q] = spec_n[q];
+        }
+        todo.swap(again);
+        e->n_fallback += (int64_t)todo.size();
+    }
     int64_t vmax = 1;
     for (int q = 0; q < nq; ++q) vmax = std::max(vmax, h_votes[q]);
     const double votes = (double)vmax;
@@ -1575,7 +1604,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // exact for heavier queries too (overflows fall back; tests/test_gpu_match_load.py) but one
     // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~540k
     // votes each) took 48.6 s on it against 1.43 s on the global path
-    const bool fast = e->k5_path == 1 || (e->k5_path == 0 && 2.0 * votes <= 65536.0);
+    const bool fast = !speculate && (e->k5_path == 1 || (e->k5_path == 0 && 2.0 * votes <= 65536.0));
     // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
     // through to the global-histogram path below
     if (fast) {
