@@ -61,7 +61,22 @@ def load_pmc(kernel: str):
     return None, None
 
 
-def cpu_baseline(host_pcm: np.ndarray) -> dict:
+def parity(eng, host_pcm: np.ndarray, ref=None) -> dict:
+    """Hashes of the bench batch (left by the last step) against the C oracle, bit for bit.
+
+    `ref` = the oracle's records for the first len(ref) clips when the cpu_baseline leg already
+    computed them; otherwise the oracle runs here on the first 8 clips."""
+    if ref is None:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle as O  # checker only
+
+        ref = O.fingerprint_batch(host_pcm[:8], 512, threads=min(8, os.cpu_count() or 1))
+    bad = [c for c in range(len(ref)) if not np.array_equal(eng.hashes(c), ref[c])]
+    return {"clips": len(ref), "hashes": int(sum(len(r) for r in ref)), "bit_exact": not bad,
+            "mismatched_clips": bad[:8], "oracle": "oracle/fp_oracle.c"}
+
+
+def cpu_baseline(host_pcm: np.ndarray) -> tuple[dict, list]:
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O  # checker / CPU baseline only
 
@@ -69,7 +84,7 @@ def cpu_baseline(host_pcm: np.ndarray) -> dict:
     sample = host_pcm[: min(len(host_pcm), 256)]
     O.fingerprint_batch(sample[:2], 512, threads=1)  # warm (tables)
     t = time.perf_counter()
-    O.fingerprint_batch(sample, 512, threads=threads)
+    ref = O.fingerprint_batch(sample, 512, threads=threads)
     dt_mt = time.perf_counter() - t
     one = sample[:16]
     t = time.perf_counter()
@@ -77,7 +92,7 @@ def cpu_baseline(host_pcm: np.ndarray) -> dict:
     dt_1 = time.perf_counter() - t
     audio_mt = sample.shape[0] * sample.shape[1] / SR
     audio_1 = one.shape[0] * one.shape[1] / SR
-    return {
+    return ref, {
         "value": round(audio_mt / dt_mt, 1),
         "unit": "audio-s/s",
         "cores": threads,
@@ -204,10 +219,14 @@ def main() -> int:
                 "64-bin blocks and K2 reads only those, so the PMC traffic can be below the algorithmic bytes",
     }
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    cpu = par = None
+    if rank == 0:
         host = pcm.view(CLIPS, n).cpu().numpy()
-        cpu = cpu_baseline(host)
+        ref = None
+        if world == 1 and not args.no_cpu:
+            ref, cpu = cpu_baseline(host)
+        # untimed: the batch's hashes (from the last step) against the oracle's
+        par = parity(eng, host, ref)
 
     if rank == 0:
         line = {
@@ -238,12 +257,13 @@ def main() -> int:
             "kernels": kern,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity": par,
         }
         print(json.dumps(line), flush=True)
     eng.close()
     if dist:
         dist.destroy_process_group()
-    return 0
+    return 0 if par is None or par["bit_exact"] else 1
 
 
 if __name__ == "__main__":
