@@ -31,7 +31,7 @@ constexpr int kK2SinkBlocks = 1024;  // K2 mask-store sinks: 256 u64 per workgro
 #define AID_K1_COMPACT 1
 #endif
 #ifndef AID_K1_E1ADDTID
-#define AID_K1_E1ADDTID 0
+#define AID_K1_E1ADDTID 1  // K1 0.2644 -> 0.2577 ms, 6.10 -> 6.21 M audio-s/s same-box (r02)
 #endif
 // float2 entries (E1: 16x68, E2: 64x17, E3: 1024; E1 by ds_write_addtid: 32 regions of 64 dwords at
 // shifted bases, 2160 dwords -- see stft.hip)

@@ -91,9 +91,37 @@
 __host__ __device__ constexpr int e1_perm(int p) { return (p & ~7) | ((p & 1) << 2) | ((p >> 1) & 3); }
 __host__ __device__ constexpr int e1_region(int k1, int c) { return 128 * k1 + 64 * c + 8 * (k1 < 8 ? k1 : k1 - 1); }
 static_assert(e1_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave, "E1 regions exceed the wave buffer");
+#endif
+// AID_K1_E3ADDTID=1 (needs AID_K1_E1ADDTID): E3 (the stage-C spill the real split reads) as 32
+// ds_write_addtid_b32 too (64 instead of 96 LDS cycles per frame). Stage-C lane L = 4 kq + mq holds
+// Z[kq + 16 j1 + 256 bitrev2(mq)] (negated for mq > 0) in register j1; component c of register j1 goes to
+// region (j1, c) at dword 130 j1 + 64 c, position L. A pair of adjacent positions then holds
+//   (4 kq, 4 kq + 1):     (Z[k], -Z[k + 512])            k = kq + 16 j1 < 256
+//   (4 kq + 2, 4 kq + 3): (-Z[k + 256], -Z[k + 768])
+// so one ds_read_b64 per component gives the real split two mirror pairs at once. Lane l, unit u < 4
+// reads, for k = l + 64 u: (Z[k], Z[k + 512]) from region 4 u + l / 16 and (Z[512 - k], Z[1024 - k]) from
+// region 4 (3 - u) + (64 - l) / 16, and computes the pairs (k, 1024 - k) and (512 - k, 512 + k): the same
+// stores of 64 consecutive bins as the layout above. Region bases 130 j1 (= 2 j1 mod 4) put the two
+// 16-lane halves of each 32-lane read group on the even / odd bank pairs: conflict-free except lane 0
+// against lane 31 in the mirror reads of u = 1..3. Bins 256 and 768 (the pair k = 256, which no unit
+// holds) are computed by every lane from one broadcast read, as bin 512 is in the layout above.
+#ifndef AID_K1_E3ADDTID
+#define AID_K1_E3ADDTID 0
+#endif
+#ifndef AID_K1_E3STAGED
+#define AID_K1_E3STAGED 0  // 1: the split's reads waited for unit by unit (counted lgkmcnt) instead of all at once
+#endif
+#if AID_K1_E3ADDTID
+static_assert(AID_K1_E1ADDTID, "AID_K1_E3ADDTID needs the add-TID E1 buffer layout");
+__host__ __device__ constexpr int e3_region(int j1, int c) { return 130 * j1 + 64 * c; }
+// highest dword read: lane 0's (unused) mirror read of unit 0, component 1
+static_assert(e3_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave && 520 * 3 + 522 + 64 + 2 <= 2 * aid::kStftLdsPerWave,
+              "E3 regions exceed the wave buffer");
+#endif
+#if AID_K1_E1ADDTID
 // 8 registers' components -> their regions (M0 = the wave buffer's LDS byte address). s_nop 0: one wait
 // state between an SALU write of M0 and an add-TID LDS instruction
-#define AID_ADDTID8(K0)                                                                                      \
+#define AID_TID8(RG, K0)                                                                                     \
     asm volatile("s_mov_b32 m0, %[base]\n\ts_nop 0\n\t"                                                      \
                  "ds_write_addtid_b32 %0 offset:%8\n\tds_write_addtid_b32 %1 offset:%9\n\t"                  \
                  "ds_write_addtid_b32 %2 offset:%10\n\tds_write_addtid_b32 %3 offset:%11\n\t"                \
@@ -101,10 +129,10 @@ static_assert(e1_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave, "E1 regions exc
                  "ds_write_addtid_b32 %6 offset:%14\n\tds_write_addtid_b32 %7 offset:%15"                    \
                  :                                                                                           \
                  : "v"(v[K0].x), "v"(v[K0].y), "v"(v[K0 + 1].x), "v"(v[K0 + 1].y), "v"(v[K0 + 2].x),         \
-                   "v"(v[K0 + 2].y), "v"(v[K0 + 3].x), "v"(v[K0 + 3].y), "i"(4 * e1_region(K0, 0)),          \
-                   "i"(4 * e1_region(K0, 1)), "i"(4 * e1_region(K0 + 1, 0)), "i"(4 * e1_region(K0 + 1, 1)),   \
-                   "i"(4 * e1_region(K0 + 2, 0)), "i"(4 * e1_region(K0 + 2, 1)), "i"(4 * e1_region(K0 + 3, 0)), \
-                   "i"(4 * e1_region(K0 + 3, 1)), [base] "s"(m0base)                                         \
+                   "v"(v[K0 + 2].y), "v"(v[K0 + 3].x), "v"(v[K0 + 3].y), "i"(4 * RG(K0, 0)),                 \
+                   "i"(4 * RG(K0, 1)), "i"(4 * RG(K0 + 1, 0)), "i"(4 * RG(K0 + 1, 1)),   \
+                   "i"(4 * RG(K0 + 2, 0)), "i"(4 * RG(K0 + 2, 1)), "i"(4 * RG(K0 + 3, 0)), \
+                   "i"(4 * RG(K0 + 3, 1)), [base] "s"(m0base)                                         \
                  : "memory", "m0")
 #endif
 // AID_K1_BRANCHFREE=1: the real split computes the row's 16 powers per lane first, then the hot word,
@@ -126,7 +154,7 @@ static_assert(e1_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave, "E1 regions exc
 #define AID_K1_TPF_A 0
 #endif
 #ifndef AID_K1_TPF_B
-#define AID_K1_TPF_B 0
+#define AID_K1_TPF_B 8  // K1 0.2657 -> 0.2619 ms same-box on top of AID_K1_E1ADDTID (r02)
 #endif
 #ifndef AID_K1_TPF_S  // 1: the real split's 24 LDS reads (E3 pairs + split twiddles) issued up front
 #define AID_K1_TPF_S 0
@@ -277,7 +305,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     //   s_tb4[h] = T64[(lane&3)*j1], j1 = 2h, 2h+1 ; s_t2p[i] = (T2K[k], T2K[1024-k]), k = lane + 64i
     __shared__ float4 s_win4[512], s_ta4[512];
 #if AID_K1_T2HALF
-    __shared__ float2 s_t2[512];  // T2K[k], k < 512
+    __shared__ float2 s_t2[512 + AID_K1_E3ADDTID];  // T2K[k], k < 512 (E3ADDTID: k <= 512)
 #else
     __shared__ float4 s_t2p[512];
 #endif
@@ -292,6 +320,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     const uint32_t m0base =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float2 *)buf);
     const uint32_t e1rd = m0base + 4u * (uint32_t)(e1_region(kq, 0) + 2 * mq);
+#endif
+#if AID_K1_E3ADDTID
+    // real-split read addresses (unit u, component c add 2080 u + 256 c, resp. 2080 (3 - u) + 256 c bytes):
+    // (Z[k], Z[k + 512]) at region 4 u + lane / 16, position 4 (lane & 15); (Z[512 - k], Z[1024 - k]) at region
+    // 4 (3 - u) + (64 - lane) / 16, position 4 ((64 - lane) & 15) + 2; (Z[256], Z[768]) at region 0, position 2
+    const uint32_t e3d = m0base + 4u * (uint32_t)(130 * (lane >> 4) + 4 * (lane & 15));
+    const uint32_t e3m = m0base + 4u * (uint32_t)(130 * ((64 - lane) >> 4) + 4 * ((64 - lane) & 15) + 2);
+    const uint32_t e3x = m0base + 8u;
 #endif
     // E3 addresses as one per-lane base + compile-time offsets (the XOR only touches bits 2-3):
     //   stage-C slot of Z[kq + 16(mq+4r) + 256 j2]: bits 4-5 of k are mq      -> e3w + 64r + 256 j2
@@ -344,6 +380,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
     }
     const float2 t512 = tab->t2k[512];
+#if AID_K1_E3ADDTID
+    if (threadIdx.x == 0) s_t2[512] = t512;
+#endif
     float2 t16[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) t16[i] = tab->t16[i];
@@ -469,10 +508,10 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 // E1: A[k1][n2] -> lane (k1 = kq, m2 = mq) gets A[kq][4*m1 + mq]
                 if (AID_K1_DIAG != 6) {
 #if AID_K1_E1ADDTID
-                    AID_ADDTID8(0);
-                    AID_ADDTID8(4);
-                    AID_ADDTID8(8);
-                    AID_ADDTID8(12);
+                    AID_TID8(e1_region, 0);
+                    AID_TID8(e1_region, 4);
+                    AID_TID8(e1_region, 8);
+                    AID_TID8(e1_region, 12);
                     {
                         // 16 ds_read_b64 in one block (hipcc would pair them into ds_read2_b64 / read2st64,
                         // 8 LDS cycles per pair instead of 2 + 2); the block waits for its own results
@@ -600,9 +639,19 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     v[j0 + 1] = make_float2(u1, w1);
                     v[j0 + 2] = make_float2(u2, w2);
                     v[j0 + 3] = make_float2(u3, w3);
+#if AID_K1_E3ADDTID
+                    if constexpr (!LOGMAG) {  // literal register groups for the asm's immediates
+                        if (j0 == 0) AID_TID8(e3_region, 0);
+                        else if (j0 == 4) AID_TID8(e3_region, 4);
+                        else if (j0 == 8) AID_TID8(e3_region, 8);
+                        else AID_TID8(e3_region, 12);
+                    } else
+#endif
+                    {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (AID_K1_DIAG != 8) buf[e3w + 16 * (j0 + j)] = v[j0 + j];
+                        for (int j = 0; j < 4; ++j)
+                            if (AID_K1_DIAG != 8) buf[e3w + 16 * (j0 + j)] = v[j0 + j];
+                    }
                 }
 #else
 #pragma unroll
@@ -646,6 +695,112 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 float *drow = dst + (int64_t)f * kBins;
 #if AID_K1_BRANCHFREE
                 if constexpr (!LOGMAG && AID_K1_DIAG == 0) {
+#if AID_K1_E3ADDTID
+                    // real split over the add-TID E3 regions (see e3_region): 18 ds_read_b64 in one block
+                    // (hipcc would pair them into 8-cycle ds_read2 forms); q[4u + 0/1] = (Z[k], -Z[k + 512])
+                    // re / im, q[4u + 2/3] = (-Z[512 - k], -Z[1024 - k]) re / im, k = lane + 64 u; x = the
+                    // broadcast (-Z[256], -Z[768])
+                    uint32_t hotw = 0;
+                    float2 q[16], qx0, qx1;
+                    asm volatile(
+                        "ds_read_b64 %0, %18 offset:0\n\tds_read_b64 %1, %18 offset:256\n\t"
+                        "ds_read_b64 %2, %19 offset:6240\n\tds_read_b64 %3, %19 offset:6496\n\t"
+                        "ds_read_b64 %4, %18 offset:2080\n\tds_read_b64 %5, %18 offset:2336\n\t"
+                        "ds_read_b64 %6, %19 offset:4160\n\tds_read_b64 %7, %19 offset:4416\n\t"
+                        "ds_read_b64 %8, %18 offset:4160\n\tds_read_b64 %9, %18 offset:4416\n\t"
+                        "ds_read_b64 %10, %19 offset:2080\n\tds_read_b64 %11, %19 offset:2336\n\t"
+                        "ds_read_b64 %12, %18 offset:6240\n\tds_read_b64 %13, %18 offset:6496\n\t"
+                        "ds_read_b64 %14, %19 offset:0\n\tds_read_b64 %15, %19 offset:256\n\t"
+                        "ds_read_b64 %16, %20 offset:0\n\tds_read_b64 %17, %20 offset:256"
+#if !AID_K1_E3STAGED
+                        "\n\ts_waitcnt lgkmcnt(0)"
+#endif
+                        : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]), "=&v"(q[6]),
+                          "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11]), "=&v"(q[12]),
+                          "=&v"(q[13]), "=&v"(q[14]), "=&v"(q[15]), "=&v"(qx0), "=&v"(qx1)
+                        : "v"(e3d), "v"(e3m), "v"(e3x)
+                        : "memory");
+                    float pa[4], pb[4], pc[4], pd[4];  // bins k, 1024 - k, 512 + k, 512 - k
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+#if AID_K1_E3STAGED
+                        // LDS reads of one wave complete in order: unit u's 4 are done once at most
+                        // 14 - 4 u of the block's reads (or later LDS ops) are outstanding
+                        if (u == 0) asm volatile("s_waitcnt lgkmcnt(14)" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]));
+                        if (u == 1) asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7]));
+                        if (u == 2) asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(q[8]), "+v"(q[9]), "+v"(q[10]), "+v"(q[11]));
+                        if (u == 3) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(q[12]), "+v"(q[13]), "+v"(q[14]), "+v"(q[15]));
+#endif
+                        const float2 dre = q[4 * u], dim = q[4 * u + 1], mre = q[4 * u + 2], mim = q[4 * u + 3];
+                        const bool l0 = u == 0 && lane == 0;  // k = 0
+                        {   // pair (k, 1024 - k): Z[1024 - k] is stored negated; k = 0 pairs with Z[0] itself
+                            const float2 a = make_float2(dre.x, dim.x);
+                            const float2 b = l0 ? a : make_float2(-mre.y, -mim.y);
+                            const float er = a.x + b.x, ei = a.y - b.y;
+                            const float orr = a.y + b.y, oi = b.x - a.x;
+                            const float2 tw = cmul(make_float2(orr, oi), s_t2[64 * u + lane]);
+                            const float xr = er + tw.x, xi = ei + tw.y;
+                            pa[u] = __builtin_fmaf(xr, xr, xi * xi);
+                            const float xr2 = er - tw.x, xi2 = tw.y - ei;  // AID_K1_MIRROR_ID
+                            pb[u] = l0 ? 0.f : __builtin_fmaf(xr2, xr2, xi2 * xi2);  // k = 0: Nyquist, dropped
+                        }
+                        {   // pair (K, 1024 - K), K = 512 - k: both stored negated (every sum flips sign, the
+                            // squares do not see it); k = 0: K = 512 is its own mirror (lane 0's mirror read
+                            // of unit 0 is not a bin)
+                            const float2 b = make_float2(dre.y, dim.y);
+                            const float2 a = l0 ? b : make_float2(mre.x, mim.x);
+                            const float er = a.x + b.x, ei = a.y - b.y;
+                            const float orr = a.y + b.y, oi = b.x - a.x;
+                            const float2 tw = cmul(make_float2(orr, oi), s_t2[512 - 64 * u - lane]);
+                            const float xr = er + tw.x, xi = ei + tw.y;
+                            pd[u] = __builtin_fmaf(xr, xr, xi * xi);
+                            const float xr2 = er - tw.x, xi2 = tw.y - ei;
+                            pc[u] = l0 ? 0.f : __builtin_fmaf(xr2, xr2, xi2 * xi2);
+                        }
+                        hotw |= __ballot(pa[u] > thr) ? 1u << u : 0u;                            // block u
+                        hotw |= __ballot(pb[u] > thr) ? (u == 0 ? 1u << 15 : 3u << (15 - u)) : 0u;  // 15-u, 16-u
+                        hotw |= __ballot(pc[u] > thr) ? 1u << (8 + u) : 0u;                      // block 8+u
+                        {  // exact bits: a superset here would mark block 8 - u hot above a hot block 7 - u
+                            const uint64_t hb = __ballot(pd[u] > thr);
+                            hotw |= (hb >> 1) ? 1u << (7 - u) : 0u;  // lanes 1..63: block 7 - u
+                            hotw |= (hb & 1) ? 1u << (8 - u) : 0u;   // lane 0: block 8 - u
+                        }
+                    }
+#if AID_K1_E3STAGED
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qx0), "+v"(qx1));
+#endif
+                    {  // bins 256 and 768: every lane (same addresses, same values)
+                        const float2 a = make_float2(qx0.x, qx1.x), b = make_float2(qx0.y, qx1.y);
+                        const float er = a.x + b.x, ei = a.y - b.y;
+                        const float orr = a.y + b.y, oi = b.x - a.x;
+                        const float2 tw = cmul(make_float2(orr, oi), s_t2[256]);
+                        const float xr = er + tw.x, xi = ei + tw.y;
+                        const float p256 = __builtin_fmaf(xr, xr, xi * xi);
+                        const float xr2 = er - tw.x, xi2 = tw.y - ei;
+                        const float p768 = __builtin_fmaf(xr2, xr2, xi2 * xi2);
+                        pstore(drow + 256, p256);
+                        pstore(drow + 768, p768);
+                        hotw |= p256 > thr ? 1u << 4 : 0u;
+                        hotw |= p768 > thr ? 1u << 12 : 0u;
+                    }
+                    hotw = __builtin_amdgcn_readfirstlane(hotw);
+                    dhot[f] = hotw;
+                    const uint32_t hsel = keep ? 0x1FFFFu : hotw;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if ((hsel >> u) & 1u) pstore(drow + lane + 64 * u, pa[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (((hsel >> (8 + u)) & 1u) && (u > 0 || lane != 0)) pstore(drow + 512 + lane + 64 * u, pc[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (((hsel >> (7 - u)) | (hsel >> (8 - u))) & 1u) pstore(drow + 512 - (lane + 64 * u), pd[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t need = (hsel >> (15 - u)) | (u > 0 ? hsel >> (16 - u) : 0u);
+                        if ((need & 1u) && (u > 0 || lane != 0)) pstore(drow + 1024 - (lane + 64 * u), pb[u]);
+                    }
+#else
                     // straight-line real split: all 16 powers first, then the hot word, then 16
                     // unconditional stores whose base is the row or, for a cold block, this
                     // workgroup's dummy row (a scalar select: no branch splits the arithmetic)
@@ -746,6 +901,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         b[1024 - (lane + 64 * i)] = pm[i];
                     }
 #endif
+#endif  // AID_K1_E3ADDTID
                 } else
 #endif
                 {
