@@ -65,7 +65,10 @@ inline int peak_strip_len(const int64_t *frames, int n, int64_t slots) {
 }
 
 // K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
-constexpr int kHashChunk = 1024;
+#ifndef AID_HASH_CHUNK
+#define AID_HASH_CHUNK 1024
+#endif
+constexpr int kHashChunk = AID_HASH_CHUNK;
 constexpr int kHashChunkPeakCap = 64 * ((kHashChunk + kZoneDT + 7) / 8);
 
 inline int64_t num_frames(int64_t n, int hop) { return (hop <= 0 || n < kN) ? 0 : 1 + (n - kN) / hop; }

@@ -122,8 +122,15 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # AIDFP_BENCH_BACKEND=gloo: rehearsal of the N-rank path on fewer GPUs than ranks (ranks share
+        # devices round-robin; RCCL refuses two ranks on one GPU). The driver's runs use RCCL, one GPU each.
+        backend = os.environ.get("AIDFP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
 
@@ -180,7 +187,8 @@ def main() -> int:
     eng.profile_enable(False)
 
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        on_dev = dist.get_backend() == "nccl"
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_dev else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
