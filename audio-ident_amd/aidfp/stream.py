@@ -47,6 +47,8 @@ class StreamIdentifier:
         self.stage = torch.empty(0, dtype=torch.float32, device="cuda")
         self.win_buf = torch.empty(0, dtype=torch.float32, device="cuda")
         self.carry = np.zeros((0, 2), dtype=np.float32)  # odd trailing frame kept for the next push
+        self._pin = None     # pinned host staging of a chunk (asynchronous H2D, about twice the pageable rate)
+        self._pin_ev = None  # recorded after the copy out of _pin: the next push waits for it before refilling
         self.filled = 0      # valid samples in self.mono
         self.base = 0        # stream sample index (index rate) of self.mono[0]; always even
         self.next_start = 0  # stream sample index of the next window
@@ -59,6 +61,20 @@ class StreamIdentifier:
             self.raw_filled = 0  # frames held
             self.n_in = 0        # frames received
             self.m_next = 0      # next output sample (index rate) to produce
+
+    def _h2d(self, dst, x: np.ndarray) -> None:
+        """dst[:n] = x (flat float32) through the pinned staging buffer, asynchronously on the current stream."""
+        import torch
+
+        n = x.size
+        if self._pin_ev is not None:
+            self._pin_ev.synchronize()  # the previous chunk has left the staging buffer
+        if self._pin is None or self._pin.numel() < n:
+            self._pin = torch.empty(n, dtype=torch.float32).pin_memory()
+            self._pin_ev = torch.cuda.Event()
+        self._pin.numpy()[:n] = x
+        dst[:n].copy_(self._pin[:n], non_blocking=True)
+        self._pin_ev.record()
 
     # -- mono buffer (index rate) --
     def _reserve_mono(self, n: int) -> None:
@@ -84,7 +100,7 @@ class StreamIdentifier:
         self._reserve_mono(n)
         if self.stage.numel() < 2 * n:
             self.stage = torch.empty(2 * n, dtype=torch.float32, device="cuda")
-        self.stage[: 2 * n].copy_(torch.from_numpy(x.reshape(-1)))
+        self._h2d(self.stage, x.reshape(-1))
         self.eng.downmix(self.stage.data_ptr(), n, self.mono.data_ptr() + 4 * self.filled, s)
         self.filled += n
 
@@ -104,7 +120,7 @@ class StreamIdentifier:
             self.raw[: 2 * keep] = self.raw[2 * drop: 2 * self.raw_filled].clone()
             self.raw_base += drop
             self.raw_filled = keep
-        self.raw[2 * self.raw_filled: 2 * (self.raw_filled + n)].copy_(torch.from_numpy(x.reshape(-1)))
+        self._h2d(self.raw[2 * self.raw_filled: 2 * (self.raw_filled + n)], x.reshape(-1))
         self.raw_filled += n
         self.n_in += n
         # outputs m whose last input floor((m*down + hl)/up) has arrived
@@ -135,14 +151,17 @@ class StreamIdentifier:
             self.next_start += self.hop
         if not starts:
             return []
-        # overlapping windows -> one contiguous clip each (device copies), one batched call
         k = len(starts)
-        if self.win_buf.numel() < k * self.win:
-            self.win_buf = torch.empty(k * self.win, dtype=torch.float32, device="cuda")
-        for i, st in enumerate(starts):
-            r = st - self.base
-            self.win_buf[i * self.win:(i + 1) * self.win] = self.mono[r:r + self.win]
-        self.eng.extract_device(self.win_buf.data_ptr(), np.arange(k + 1, dtype=np.int64) * self.win, s)
+        offs = np.arange(k + 1, dtype=np.int64) * self.win
+        if k == 1:  # one window (a push of <= one hop): extract it in place (even start: 8-B aligned)
+            self.eng.extract_device(self.mono.data_ptr() + 4 * (starts[0] - self.base), offs, s)
+        else:  # overlapping windows -> one contiguous clip each (device copies), one batched call
+            if self.win_buf.numel() < k * self.win:
+                self.win_buf = torch.empty(k * self.win, dtype=torch.float32, device="cuda")
+            for i, st in enumerate(starts):
+                r = st - self.base
+                self.win_buf[i * self.win:(i + 1) * self.win] = self.mono[r:r + self.win]
+            self.eng.extract_device(self.win_buf.data_ptr(), offs, s)
         rows = self.eng.query_extracted()
         return [WindowResult(st / self.sr, r) for st, r in zip(starts, rows)]
 
