@@ -117,10 +117,11 @@ __device__ __forceinline__ void dft4_pk(float2 &a, float2 &b, float2 &c, float2 
 
 // FPSPEC 3 DFT16: v[16] in natural input order -> out[c + 4d] in v (natural output order).
 // t16 holds W16^1, W16^2, W16^3, W16^4 (unused), W16^6, W16^9 at indices 1,2,3,4,6,9.
-__device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10]) {
+// b0 > 0: the caller already ran the first-round DFT4s of b < b0 (staged E1 reads in K1)
+__device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10], const int b0 = 0) {
     // s[b][c] lives in v[b + 4c] after the first DFT4 over (b, b+4, b+8, b+12)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = b0; b < 4; ++b) {
         if (AID_PK_DFT4) dft4_pk(v[b], v[b + 4], v[b + 8], v[b + 12]);
         else dft4(v[b], v[b + 4], v[b + 8], v[b + 12]);
     }

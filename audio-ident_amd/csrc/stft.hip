@@ -87,6 +87,9 @@
 //     readers kq of one 32-lane group then hit 8 distinct 8-bank slots (ds_read_b64: 64 banks).
 // Reads are 16 ds_read_b64 (2 cycles each, as the 8 ds_read_b128 before). 2160 dwords per wave: 16 waves
 // + the tables take 159,232 of the 163,840 LDS bytes.
+#ifndef AID_K1_E1STAGED
+#define AID_K1_E1STAGED 0  // 1: E1 reads in two blocks; stage B's first two DFT4s run while the second lands
+#endif
 #if AID_K1_E1ADDTID
 __host__ __device__ constexpr int e1_perm(int p) { return (p & ~7) | ((p & 1) << 2) | ((p >> 1) & 3); }
 __host__ __device__ constexpr int e1_region(int k1, int c) { return 128 * k1 + 64 * c + 8 * (k1 < 8 ? k1 : k1 - 1); }
@@ -512,6 +515,57 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     AID_TID8(e1_region, 4);
                     AID_TID8(e1_region, 8);
                     AID_TID8(e1_region, 12);
+#if AID_K1_E1STAGED
+                    {
+                        // the reads of m1 = 0, 1, 4, 5, 8, 9, 12, 13 (j even) first: once they are in (8 later
+                        // reads outstanding), stage B's first-round DFT4s over b = 0, 1 run while the rest land
+                        float2 qa[8], qb[8];
+                        asm volatile(
+                            "ds_read_b64 %0, %8 offset:0\n\tds_read_b64 %1, %8 offset:256\n\t"
+                            "ds_read_b64 %2, %8 offset:64\n\tds_read_b64 %3, %8 offset:320\n\t"
+                            "ds_read_b64 %4, %8 offset:128\n\tds_read_b64 %5, %8 offset:384\n\t"
+                            "ds_read_b64 %6, %8 offset:192\n\tds_read_b64 %7, %8 offset:448"
+                            : "=&v"(qa[0]), "=&v"(qa[1]), "=&v"(qa[2]), "=&v"(qa[3]), "=&v"(qa[4]), "=&v"(qa[5]),
+                              "=&v"(qa[6]), "=&v"(qa[7])
+                            : "v"(e1rd)
+                            : "memory");
+                        asm volatile(
+                            "ds_read_b64 %0, %8 offset:32\n\tds_read_b64 %1, %8 offset:288\n\t"
+                            "ds_read_b64 %2, %8 offset:96\n\tds_read_b64 %3, %8 offset:352\n\t"
+                            "ds_read_b64 %4, %8 offset:160\n\tds_read_b64 %5, %8 offset:416\n\t"
+                            "ds_read_b64 %6, %8 offset:224\n\tds_read_b64 %7, %8 offset:480"
+                            : "=&v"(qb[0]), "=&v"(qb[1]), "=&v"(qb[2]), "=&v"(qb[3]), "=&v"(qb[4]), "=&v"(qb[5]),
+                              "=&v"(qb[6]), "=&v"(qb[7])
+                            : "v"(e1rd)
+                            : "memory");
+                        // a wave's LDS reads complete in order: <= 8 outstanding = the first block is in
+                        asm volatile("s_waitcnt lgkmcnt(8)"
+                                     : "+v"(qa[0]), "+v"(qa[1]), "+v"(qa[2]), "+v"(qa[3]), "+v"(qa[4]), "+v"(qa[5]),
+                                       "+v"(qa[6]), "+v"(qa[7])
+                                     :
+                                     : "memory");
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {  // j = 2 jj
+                            v[4 * jj] = make_float2(qa[2 * jj].x, qa[2 * jj + 1].x);
+                            v[4 * jj + 1] = make_float2(qa[2 * jj].y, qa[2 * jj + 1].y);
+                        }
+                        if (AID_K1_DIAG != 9) {
+                            dft4(v[0], v[4], v[8], v[12]);
+                            dft4(v[1], v[5], v[9], v[13]);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        asm volatile("s_waitcnt lgkmcnt(0)"
+                                     : "+v"(qb[0]), "+v"(qb[1]), "+v"(qb[2]), "+v"(qb[3]), "+v"(qb[4]), "+v"(qb[5]),
+                                       "+v"(qb[6]), "+v"(qb[7])
+                                     :
+                                     : "memory");
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {  // j = 2 jj + 1
+                            v[4 * jj + 2] = make_float2(qb[2 * jj].x, qb[2 * jj + 1].x);
+                            v[4 * jj + 3] = make_float2(qb[2 * jj].y, qb[2 * jj + 1].y);
+                        }
+                    }
+#else
                     {
                         // 16 ds_read_b64 in one block (hipcc would pair them into ds_read2_b64 / read2st64,
                         // 8 LDS cycles per pair instead of 2 + 2); the block waits for its own results
@@ -538,6 +592,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                             v[2 * j + 1] = make_float2(q[2 * j].y, q[2 * j + 1].y);
                         }
                     }
+#endif  // AID_K1_E1STAGED
 #elif AID_K1_E1SWAP
                     e1_transpose(v);
 #elif AID_K1_E1V
@@ -575,7 +630,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 for (int h = 0; h < AID_K1_TPF_B; ++h) tpb[h] = s_tb4[4 * h + mq];
                 __builtin_amdgcn_sched_barrier(0);
 #endif
-                if (AID_K1_DIAG != 9) dft16(v, t16);
+                if (AID_K1_DIAG != 9) dft16(v, t16, AID_K1_E1ADDTID && AID_K1_E1STAGED ? 2 : 0);
 #if AID_K1_TPF_B
 #pragma unroll
                 for (int h = AID_K1_TPF_B; h < 8; ++h) tpb[h] = s_tb4[4 * h + mq];
