@@ -28,11 +28,19 @@ struct ExactRow {  // == aid_exact_row (include/aidfp.h)
 
 __global__ __launch_bounds__(256) void k_window_gather(const float *__restrict__ src, const int64_t *__restrict__ win,
                                                        int n_win, float *__restrict__ dst) {
-    // win[3*w] = source offset, win[3*w+1] = length, win[3*w+2] = destination offset (even)
+    // win[3*w] = source offset, win[3*w+1] = length (even), win[3*w+2] = destination offset (even): float2
+    // stores; float2 loads when the source is 8-B aligned too (every other window at 44.1 kHz starts odd)
     for (int w = blockIdx.y; w < n_win; w += gridDim.y) {
-        const int64_t so = win[3 * w], n = win[3 * w + 1], d = win[3 * w + 2];
-        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-            dst[d + i] = src[so + i];
+        const int64_t so = win[3 * w], n2 = win[3 * w + 1] >> 1, d = win[3 * w + 2];
+        float2 *__restrict__ d2 = reinterpret_cast<float2 *>(dst + d);
+        const float *s = src + so;
+        const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+        if ((reinterpret_cast<uintptr_t>(s) & 7) == 0) {
+            const float2 *__restrict__ s2 = reinterpret_cast<const float2 *>(s);
+            for (int64_t i = i0; i < n2; i += step) d2[i] = s2[i];
+        } else {
+            for (int64_t i = i0; i < n2; i += step) d2[i] = make_float2(s[2 * i], s[2 * i + 1]);
+        }
     }
 }
 
