@@ -122,6 +122,7 @@ static_assert(e3_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave && 520 * 3 + 522
               "E3 regions exceed the wave buffer");
 #endif
 #if AID_K1_E1ADDTID
+__host__ __device__ constexpr int e2_region(int j1, int c) { return 128 * j1 + 64 * c; }  // AID_K1_DPPC 3
 // 8 registers' components -> their regions (M0 = the wave buffer's LDS byte address). s_nop 0: one wait
 // state between an SALU write of M0 and an add-TID LDS instruction
 #define AID_TID8(RG, K0)                                                                                     \
@@ -323,6 +324,15 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     const uint32_t m0base =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float2 *)buf);
     const uint32_t e1rd = m0base + 4u * (uint32_t)(e1_region(kq, 0) + 2 * mq);
+#endif
+#if AID_K1_DPPC == 3
+    // E2 reader lane: kq2 = lane & 15, s = lane >> 4 (regions j1 = 4 s + r); its E3 slots e3(kq2 + 16 (4 s + r) +
+    // 256 j2) = e3c[j2] + 16 r + 256 j2 (the E3 swizzle flips bits 2-3 of kq2 by bits 8-9 = j2)
+    static_assert(AID_K1_E1ADDTID, "AID_K1_DPPC 3 writes E2 by add-TID");
+    const uint32_t e2rd = m0base + 4u * (uint32_t)(512 * (lane >> 4) + 4 * (lane & 15));
+    int e3c[4];
+#pragma unroll
+    for (int j2 = 0; j2 < 4; ++j2) e3c[j2] = e3((lane & 15) + 64 * (lane >> 4) + 256 * j2) - 256 * j2;
 #endif
 #if AID_K1_E3ADDTID
     // real-split read addresses (unit u, component c add 2080 u + 256 c, resp. 2080 (3 - u) + 256 c bytes):
@@ -653,7 +663,43 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 //   s2 = (+1, -1, -1, +1): lanes 0..3 -> y0, -y2, -y1, -y3
                 // fma(p, +-1, x) rounds x +- p once: FPSPEC's add/sub values; the signs are exact
                 // and cancel in the real split (see there)
-#if AID_K1_DPPC == 2
+#if AID_K1_DPPC == 3
+                {
+                    // E2 by add-TID: lane (kq, mq) puts component c of B[kq][mq][j1] at position 4 kq + mq of
+                    // region (j1, c) = dword 128 j1 + 64 c; reader lane l (kq2 = l & 15, s = l >> 4) takes the
+                    // 4 m2 values of B[kq2][.][4 s + r] as one ds_read_b128 per component (conflict-free: the 16
+                    // lanes of each b128 group cover 16 distinct 4-bank quads), runs FPSPEC 3's DFT4 in
+                    // registers and spills Z[kq2 + 16 (4 s + r) + 256 j2] (true signs) to E3
+                    AID_TID8(e2_region, 0);
+                    AID_TID8(e2_region, 4);
+                    AID_TID8(e2_region, 8);
+                    AID_TID8(e2_region, 12);
+                    float4 q2[8];
+                    asm volatile(
+                        "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:256\n\t"
+                        "ds_read_b128 %2, %8 offset:512\n\tds_read_b128 %3, %8 offset:768\n\t"
+                        "ds_read_b128 %4, %8 offset:1024\n\tds_read_b128 %5, %8 offset:1280\n\t"
+                        "ds_read_b128 %6, %8 offset:1536\n\tds_read_b128 %7, %8 offset:1792\n\t"
+                        "s_waitcnt lgkmcnt(0)"
+                        : "=&v"(q2[0]), "=&v"(q2[1]), "=&v"(q2[2]), "=&v"(q2[3]), "=&v"(q2[4]), "=&v"(q2[5]),
+                          "=&v"(q2[6]), "=&v"(q2[7])
+                        : "v"(e2rd)
+                        : "memory");
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float4 re = q2[2 * r], im = q2[2 * r + 1];
+                        float2 x0 = make_float2(re.x, im.x), x1 = make_float2(re.y, im.y);
+                        float2 x2 = make_float2(re.z, im.z), x3 = make_float2(re.w, im.w);
+                        dft4(x0, x1, x2, x3);
+                        if (AID_K1_DIAG != 8) {
+                            buf[e3c[0] + 16 * r] = x0;
+                            buf[e3c[1] + 16 * r + 256] = x1;
+                            buf[e3c[2] + 16 * r + 512] = x2;
+                            buf[e3c[3] + 16 * r + 768] = x3;
+                        }
+                    }
+                }
+#elif AID_K1_DPPC == 2
                 // hand-placed: v_fmac_f32_dpp (partner * s + x, in place) keeps the DPP inside the
                 // fma; the leading s_nop 1 covers the VALU-write -> DPP-read hazard of the block's
                 // inputs, and every other DPP source was written >= 2 instructions earlier
@@ -881,7 +927,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const int bi = (i == 0 && lane == 0) ? 0 : AID_E3B(i) + 64 * (15 - i);
                         const float2 bs = buf[bi];
 #endif
-                        const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
+                        const float2 b = AID_K1_DPPC == 3 ? bs : i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
                         const float er = a.x + b.x, ei = a.y - b.y;
                         const float orr = a.y + b.y, oi = b.x - a.x;
 #if AID_K1_TPF_S
@@ -986,7 +1032,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     // and b is stored negated (except Z[0] for lane 0, i = 0), so flip b; for i >= 4 both
                     // are negated, every sum below flips sign and the squares in P do not see it
                     const float2 bs = AID_K1_DIAG == 8 ? v[15 - i] : buf[bi];
-                    const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
+                    const float2 b = AID_K1_DPPC == 3 ? bs : i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
 #else
                     const float2 b = AID_K1_DIAG == 8 ? v[15 - i] : buf[AID_K1_DIAG == 2 ? e3(k ^ 512) : bi];
 #endif
