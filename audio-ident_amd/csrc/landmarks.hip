@@ -26,6 +26,10 @@
 namespace aid {
 
 constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
+#ifndef AID_K3_KEEPW
+#define AID_K3_KEEPW 0  // 1: phase 1's mask words stay in registers for phase 2 (<= kK3MaxPer frames per thread)
+#endif
+constexpr int kK3MaxPer = (kHashChunk + kZoneDT + kK3 - 1) / kK3;  // frames per thread in phase 1, at most
 
 #ifndef AID_K3_SKIP0
 #define AID_K3_SKIP0 1  // skip the unshuffle of peak-free frames and of empty 256-bin ballot blocks
@@ -171,6 +175,24 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     }
     __syncthreads();
     for (int f = fa; f < fz; ++f) mine += foff[f];
+#elif AID_K3_KEEPW
+    // the thread's frames' mask words stay in registers for phase 2 (no second round trip to L2/MALL)
+    uint64_t KW[kK3MaxPer][kMaskWords];
+#pragma unroll
+    for (int ff = 0; ff < kK3MaxPer; ++ff) {
+        const int f = fa + ff;
+#pragma unroll
+        for (int w = 0; w < kMaskWords; ++w) KW[ff][w] = f < fz ? Mc[f * kMaskWords + w] : 0ull;
+    }
+#pragma unroll
+    for (int ff = 0; ff < kK3MaxPer; ++ff) {
+        const int f = fa + ff;
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < kMaskWords; ++w) c += __popcll(KW[ff][w]);
+        if (f < fz) foff[f] = c;
+        mine += c;
+    }
 #else
     for (int f = fa; f < fz; ++f) {
         uint32_t c = 0;
@@ -184,7 +206,14 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     int64_t run = block_excl_scan(mine, scan_tmp, &npk);
     if (AID_K3_DIAG == 1) return;  // timing only: phase 1 (counts + scan)
     // 2. expand to the (t,k)-ordered peak list (unshuffling K2's ballot layout)
+#if AID_K3_KEEPW && !AID_K3_COALESCED
+#pragma unroll
+    for (int ff = 0; ff < kK3MaxPer; ++ff) {
+        const int f = fa + ff;
+        if (f >= fz) break;
+#else
     for (int f = fa; f < fz; ++f) {
+#endif
         const uint32_t c = foff[f];
         foff[f] = (uint32_t)run;
 #if AID_K3_SKIP0
@@ -195,7 +224,12 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
         int64_t idx = run;
         uint64_t W[kMaskWords];
 #pragma unroll
-        for (int w = 0; w < kMaskWords; ++w) W[w] = Mc[f * kMaskWords + w];
+        for (int w = 0; w < kMaskWords; ++w)
+#if AID_K3_KEEPW && !AID_K3_COALESCED
+            W[w] = KW[ff][w];
+#else
+            W[w] = Mc[f * kMaskWords + w];
+#endif
 #if AID_K3_SPARSE
         // no unshuffle: a 4-bin group holds at most one peak (FPSPEC 5: no two peaks within +-15 bins), so the
         // OR of a 256-bin block's 4 ballot words has one bit per peak, in ascending bin order; the word
