@@ -90,9 +90,21 @@
 #ifndef AID_K1_E1STAGED
 #define AID_K1_E1STAGED 0  // 1: E1 reads in two blocks; stage B's first two DFT4s run while the second lands
 #endif
-#if AID_K1_E1ADDTID
+#ifndef AID_K1_E1Q
+#define AID_K1_E1Q 1  // E1 read side as 8 ds_read_b128 (see below): K1 -0.6 % and -2.4 % in two same-box A/Bs (r02)
+#endif
+#if AID_K1_E1ADDTID && AID_K1_E1Q
+// AID_K1_E1Q: stage-A lane p holds n2 = 4 (p & 15) + (p >> 4), so a stage-B reader (kq, mq) finds n2 = 4 m1 + mq for
+// m1 = 4t .. 4t+3 at positions 16 mq + 4t .. +3 of region (kq, c): one ds_read_b128 per (t, c), 8 per frame instead
+// of 16 ds_read_b64 (same LDS cycles). Region bases 128 k1 + 64 c + 4 (k1 & 3) + 16 (k1 >> 2) (2108 dwords) put the
+// 16 lanes of every b128 lane group on 16 distinct 4-bank quads
+__host__ __device__ constexpr int e1_perm(int p) { return 4 * (p & 15) + (p >> 4); }
+__host__ __device__ constexpr int e1_region(int k1, int c) { return 128 * k1 + 64 * c + 4 * (k1 & 3) + 16 * (k1 >> 2); }
+#elif AID_K1_E1ADDTID
 __host__ __device__ constexpr int e1_perm(int p) { return (p & ~7) | ((p & 1) << 2) | ((p >> 1) & 3); }
 __host__ __device__ constexpr int e1_region(int k1, int c) { return 128 * k1 + 64 * c + 8 * (k1 < 8 ? k1 : k1 - 1); }
+#endif
+#if AID_K1_E1ADDTID
 static_assert(e1_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave, "E1 regions exceed the wave buffer");
 #endif
 // AID_K1_E3ADDTID=1 (needs AID_K1_E1ADDTID): E3 (the stage-C spill the real split reads) as 32
@@ -323,7 +335,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     // LDS byte address of this wave's buffer (M0 of the add-TID writes) and of the lane's E1 reads
     const uint32_t m0base =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float2 *)buf);
+#if AID_K1_E1Q
+    const uint32_t e1rd = m0base + 4u * (uint32_t)(e1_region(kq, 0) + 16 * mq);
+#else
     const uint32_t e1rd = m0base + 4u * (uint32_t)(e1_region(kq, 0) + 2 * mq);
+#endif
 #endif
 #if AID_K1_DPPC == 3
     // E2 reader lane: kq2 = lane & 15, s = lane >> 4 (regions j1 = 4 s + r); its E3 slots e3(kq2 + 16 (4 s + r) +
@@ -525,7 +541,29 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     AID_TID8(e1_region, 4);
                     AID_TID8(e1_region, 8);
                     AID_TID8(e1_region, 12);
-#if AID_K1_E1STAGED
+#if AID_K1_E1Q
+                    {
+                        float4 q[8];  // q[2 t + c] = component c of A[kq][4 m1 + mq], m1 = 4t .. 4t+3
+                        asm volatile(
+                            "ds_read_b128 %0, %8 offset:0\n\tds_read_b128 %1, %8 offset:256\n\t"
+                            "ds_read_b128 %2, %8 offset:16\n\tds_read_b128 %3, %8 offset:272\n\t"
+                            "ds_read_b128 %4, %8 offset:32\n\tds_read_b128 %5, %8 offset:288\n\t"
+                            "ds_read_b128 %6, %8 offset:48\n\tds_read_b128 %7, %8 offset:304\n\t"
+                            "s_waitcnt lgkmcnt(0)"
+                            : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]),
+                              "=&v"(q[6]), "=&v"(q[7])
+                            : "v"(e1rd)
+                            : "memory");
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const float4 re = q[2 * t], im = q[2 * t + 1];
+                            v[4 * t] = make_float2(re.x, im.x);
+                            v[4 * t + 1] = make_float2(re.y, im.y);
+                            v[4 * t + 2] = make_float2(re.z, im.z);
+                            v[4 * t + 3] = make_float2(re.w, im.w);
+                        }
+                    }
+#elif AID_K1_E1STAGED
                     {
                         // the reads of m1 = 0, 1, 4, 5, 8, 9, 12, 13 (j even) first: once they are in (8 later
                         // reads outstanding), stage B's first-round DFT4s over b = 0, 1 run while the rest land
@@ -640,7 +678,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 for (int h = 0; h < AID_K1_TPF_B; ++h) tpb[h] = s_tb4[4 * h + mq];
                 __builtin_amdgcn_sched_barrier(0);
 #endif
-                if (AID_K1_DIAG != 9) dft16(v, t16, AID_K1_E1ADDTID && AID_K1_E1STAGED ? 2 : 0);
+                if (AID_K1_DIAG != 9) dft16(v, t16, AID_K1_E1ADDTID && AID_K1_E1STAGED && !AID_K1_E1Q ? 2 : 0);
 #if AID_K1_TPF_B
 #pragma unroll
                 for (int h = AID_K1_TPF_B; h < 8; ++h) tpb[h] = s_tb4[4 * h + mq];
