@@ -221,6 +221,15 @@ __device__ __forceinline__ void pstore(float *p, float v) {
 // mirrors stay conflict-free too (lane 0 aside). (Bit 4 ^= bit 9 alone left the writes 4-way:
 // 34 % of K1's LDS cycles were conflicts; bits 3/4 from bits 8/9 still 2-way.)
 __device__ __forceinline__ int e3(int k) { return k ^ (((k >> 9) & 1) << 2) ^ (((k >> 8) & 1) << 3); }
+// AID_K1_E3Q=1: E3 slot of Z[k] = 4 (k & 255) + (j2 ^ 2 h), j2 = k >> 8, h = bit 3 of k: the four Z[k + 256 j2]
+// sit in one 32-B group with the (j2 = 0, 1) and (2, 3) halves swapped by bit 3, so the real split reads
+// (Z[k], Z[k + 256]) and (Z[768 - k], Z[1024 - k]) as one ds_read_b128 each (8 instead of 16 ds_read_b64 per frame;
+// stage-C writers and both readers conflict-free, checked exhaustively). Lane 0's unit-0 mirror read lands on a
+// copy of slots 2, 3 (Z[512], Z[768]) at 1026, 1027, written by lanes 1 and 3 of stage C.
+#ifndef AID_K1_E3Q_DUP
+#define AID_K1_E3Q_DUP 1  // diagnostic: 0 drops the copy (wrong results for bins 768 of lane 0)
+#endif
+__device__ __forceinline__ int e3q_slot(int k) { return 4 * (k & 255) + ((k >> 8) ^ (2 * ((k >> 3) & 1))); }
 // partner value across the lane quad (DPP quad_perm; every lane of the quad is valid)
 template <int CTRL>
 __device__ __forceinline__ float quad_dpp(float x) {
@@ -368,6 +377,15 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     const int j2q = ((mq & 1) << 1) | (mq >> 1);  // lane mq holds output j2 = bitrev2(mq)
     // writer slots: e3(kq + 16 j1 + 256 j2) = (kq ^ 4 (j2 >> 1) ^ 8 (j2 & 1)) + 256 j2 + 16 j1
     const int e3w = (kq ^ (((j2q >> 1) << 2) | ((j2q & 1) << 3))) + 256 * j2q;
+#if AID_K1_E3Q
+    static_assert(AID_K1_DPPC == 2, "AID_K1_E3Q is laid out for the DPP stage C");
+    const int e3wq = 4 * kq + (j2q ^ (2 * ((kq >> 3) & 1)));  // + 64 j1
+    // split reads (float4 units): (Z[k], Z[k + 256]) at 2 k + h(k), (Z[768 - k], Z[1024 - k]) at 2 m + 1 - h(m),
+    // m = 256 - k, k = lane + 64 i (i < 4; the i terms are immediates)
+    const int e3qa = 2 * lane + ((lane >> 3) & 1);
+    const int e3qb = 513 - 2 * lane - (((256 - lane) >> 3) & 1);
+    const int e3dup = (lane == 1 || lane == 3) ? 1026 + (lane >> 1) : 1028 + lane;  // < kStftLdsPerWave (1092)
+#endif
     // readers: Z[lane + 64 i] (i < 8: bit 9 clear, bit 8 = i >> 2) -> e3a[i >> 2] + 64 i;
     // Z[1024 - lane - 64 i] = Z[64 (15 - i) + m], m = 64 - lane (bit 9 set, bit 8 = i < 4)
     //   -> e3b[i < 4] + 64 (15 - i); lane 0 (m = 64, Z[64 (16 - i)]) matches that except at i = 4
@@ -789,7 +807,18 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            if (AID_K1_DIAG != 8) buf[e3w + 16 * (j0 + j)] = v[j0 + j];
+                            if (AID_K1_DIAG != 8) buf[
+#if AID_K1_E3Q
+                                    e3wq + 64 * (j0 + j)
+#else
+                                    e3w + 16 * (j0 + j)
+#endif
+                            ] = v[j0 + j];
+#if AID_K1_E3Q
+                        // Z[512], Z[768] (lanes 1, 3) copied to 1026, 1027; every other lane to its own dummy slot: one
+                        // unconditional store (an exec-masked branch here made hipcc spill)
+                        if (AID_K1_E3Q_DUP && j0 == 0) buf[e3dup] = v[0];
+#endif
                     }
                 }
 #else
@@ -956,8 +985,26 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     }
                     __builtin_amdgcn_sched_barrier(0);
 #endif
+#if AID_K1_E3Q
+                    float4 qa, qb;  // the pair of b128 reads that serve bins i and i + 4
+#endif
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) {
+                    for (int ii = 0; ii < 8; ++ii) {
+#if AID_K1_E3Q
+                        // order i = 0, 4, 1, 5, ...: one pair of reads serves two mirror pairs, then dies
+                        const int i = (ii >> 1) + 4 * (ii & 1);
+                        if ((ii & 1) == 0) {
+                            const float4 *buf4 = reinterpret_cast<const float4 *>(buf);
+                            qa = buf4[e3qa + 128 * (ii >> 1)];
+                            qb = buf4[e3qb - 128 * (ii >> 1)];
+                        }
+                        // i < 4: a = Z[k], bs = -Z[1024 - k] (stored); i >= 4: a = -Z[k], bs = -Z[1024 - k] (k >= 256)
+                        const float2 a = i < 4 ? make_float2(qa.x, qa.y) : make_float2(qa.z, qa.w);
+                        const float2 bs = i < 4 ? make_float2(qb.z, qb.w) : make_float2(qb.x, qb.y);
+                        // k = 0 (lane 0, i = 0) pairs with Z[0] itself
+                        const float2 b = i == 0 ? (lane == 0 ? a : make_float2(-bs.x, -bs.y)) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
+#else
+                        const int i = ii;
 #if AID_K1_TPF_S
                         const float2 a = sa[i], bs = sb[i];
 #else
@@ -966,6 +1013,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float2 bs = buf[bi];
 #endif
                         const float2 b = AID_K1_DPPC == 3 ? bs : i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
+#endif
                         const float er = a.x + b.x, ei = a.y - b.y;
                         const float orr = a.y + b.y, oi = b.x - a.x;
 #if AID_K1_TPF_S
@@ -1001,7 +1049,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     }
                     {  // bin 512 pairs with itself: every lane computes it (same address, same value),
                        // so its store and the hot word's need no lane-0 branch
-                        const float2 a = buf[e3(512)];
+                        const float2 a = buf[AID_K1_E3Q ? 2 : e3(512)];
                         const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
                         const float2 tw = cmul(make_float2(orr, oi), t512);
                         const float xr = er + tw.x, xi = ei + tw.y;
@@ -1057,9 +1105,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 for (int i = 0; i < 8; ++i) {
                     const int k = lane + 64 * i;  // 0..511
 #if AID_K1_DPPC
-                    const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[(i < 4 ? e3a0 : e3a1) + 64 * i];
+                    const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[AID_K1_E3Q ? e3q_slot(k) : (i < 4 ? e3a0 : e3a1) + 64 * i];
                     // k = 0 mirrors onto itself (Z[0]: slot 0)
-                    const int bi = (i == 0 && lane == 0) ? 0 : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
+                    const int bi = (i == 0 && lane == 0) ? 0 : AID_K1_E3Q ? e3q_slot(1024 - k) : (i < 4 ? e3b1 : i == 4 ? e3b4 : e3b0) + 64 * (15 - i);
 #else
                     const float2 a = AID_K1_DIAG == 8 ? v[i] : buf[e3a + 64 * i];
                     // k = 0 mirrors onto itself (Z[0]): lane 0's e3b + 960 would be slot 1024
@@ -1125,7 +1173,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                             make_float4(pv11[4 * q], pv11[4 * q + 1], pv11[4 * q + 2], pv11[4 * q + 3]);
                 }
                 if (lane == 0) {  // bin 512 pairs with itself
-                    const float2 a = buf[e3(512)];
+                    const float2 a = buf[AID_K1_E3Q ? 2 : e3(512)];
                     const float er = a.x + a.x, ei = a.y - a.y, orr = a.y + a.y, oi = a.x - a.x;
                     const float2 tw = cmul(make_float2(orr, oi), t512);
                     const float xr = er + tw.x, xi = ei + tw.y;
