@@ -36,7 +36,7 @@ constexpr int kK2SinkBlocks = 1024;  // K2 mask-store sinks: 256 u64 per workgro
 // float2 entries (E1: 16x68, E2: 64x17, E3: 1024; E1 by ds_write_addtid: 32 regions of 64 dwords at
 // shifted bases, 2160 dwords -- see stft.hip)
 #ifndef AID_K1_E3Q
-#define AID_K1_E3Q 0  // stft.hip: E3 slots in 32-B groups of Z[k + 256 j2] (+64 dummy slots for one copy store)
+#define AID_K1_E3Q 1  // K1 -0.5 % / -0.3 % in two same-box A/Bs (r02). stft.hip: E3 slots in 32-B groups of Z[k + 256 j2] (+64 dummy slots for one copy store)
 #endif
 constexpr int kStftLdsPerWave = AID_K1_E3Q ? 1092 : AID_K1_E1ADDTID ? 1080 : AID_K1_COMPACT ? 1024 : 1088;
 

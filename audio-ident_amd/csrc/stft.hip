@@ -225,7 +225,7 @@ __device__ __forceinline__ int e3(int k) { return k ^ (((k >> 9) & 1) << 2) ^ ((
 // sit in one 32-B group with the (j2 = 0, 1) and (2, 3) halves swapped by bit 3, so the real split reads
 // (Z[k], Z[k + 256]) and (Z[768 - k], Z[1024 - k]) as one ds_read_b128 each (8 instead of 16 ds_read_b64 per frame;
 // stage-C writers and both readers conflict-free, checked exhaustively). Lane 0's unit-0 mirror read lands on a
-// copy of slots 2, 3 (Z[512], Z[768]) at 1026, 1027, written by lanes 1 and 3 of stage C.
+// copy of Z[768] at slot 1026, written by lane 3 of stage C.
 #ifndef AID_K1_E3Q_DUP
 #define AID_K1_E3Q_DUP 1  // diagnostic: 0 drops the copy (wrong results for bins 768 of lane 0)
 #endif
@@ -384,7 +384,9 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     // m = 256 - k, k = lane + 64 i (i < 4; the i terms are immediates)
     const int e3qa = 2 * lane + ((lane >> 3) & 1);
     const int e3qb = 513 - 2 * lane - (((256 - lane) >> 3) & 1);
-    const int e3dup = (lane == 1 || lane == 3) ? 1026 + (lane >> 1) : 1028 + lane;  // < kStftLdsPerWave (1092)
+    // lane 0's unit-0 mirror read (m = 256) takes slots 1026, 1027 as (Z[768 - 0], Z[1024 - 0]): Z[768] (stage-C lane 3,
+    // register 0) is copied to 1026; slot 1027 (Z[0]) is not used (k = 0 pairs with Z[0] from its own read)
+    const int e3dup = lane == 3 ? 1026 : 1028 + lane;  // < kStftLdsPerWave (1092)
 #endif
     // readers: Z[lane + 64 i] (i < 8: bit 9 clear, bit 8 = i >> 2) -> e3a[i >> 2] + 64 i;
     // Z[1024 - lane - 64 i] = Z[64 (15 - i) + m], m = 64 - lane (bit 9 set, bit 8 = i < 4)
@@ -815,8 +817,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 #endif
                             ] = v[j0 + j];
 #if AID_K1_E3Q
-                        // Z[512], Z[768] (lanes 1, 3) copied to 1026, 1027; every other lane to its own dummy slot: one
-                        // unconditional store (an exec-masked branch here made hipcc spill)
+                        // Z[768] (lane 3) copied to 1026, every other lane to its own dummy slot: one unconditional
+                        // store (an exec-masked branch here made hipcc spill)
                         if (AID_K1_E3Q_DUP && j0 == 0) buf[e3dup] = v[0];
 #endif
                     }
