@@ -20,6 +20,7 @@ AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
 AID_FLAG_KEEP_POWER = 1
+AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD = 1, 2, 3, 4, 5
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
 AID_K_COUNT = 8
 KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample",
@@ -83,6 +84,7 @@ SIGNATURES = [
     ("aid_engine_create", ctypes.c_int, [P, P]),
     ("aid_engine_destroy", None, [P]),
     ("aid_engine_config", ctypes.c_int, [P, P]),
+    ("aid_engine_force", ctypes.c_int, [P, I32, I32]),
     ("aid_num_frames", I64, [P, I64]),
     ("aid_hash_capacity", I64, [P, I64]),
     ("aid_extract", ctypes.c_int, [P, P, P, I32, I32, P]),
@@ -94,6 +96,7 @@ SIGNATURES = [
     ("aid_result_peakmask", ctypes.c_int, [P, I32, P, I64]),
     ("aid_spectrogram", ctypes.c_int, [P, P, I64, P, I64]),
     ("aid_synth", ctypes.c_int, [P, P, P, P, I32, I64, I32, ctypes.c_uint32, P]),
+    ("aid_synth_band", ctypes.c_int, [P, P, P, P, I32, I64, I32, ctypes.c_uint32, I32, P]),
     ("aid_index_reset", ctypes.c_int, [P]),
     ("aid_index_add_extracted", ctypes.c_int, [P, P]),
     ("aid_index_add_postings", ctypes.c_int, [P, P, P, P, I64, I32]),
@@ -107,10 +110,15 @@ SIGNATURES = [
     ("aid_comm_create", ctypes.c_int, [P, P, I32, I32, P]),
     ("aid_comm_destroy", None, [P]),
     ("aid_index_allgather", ctypes.c_int, [P, P, I64, P]),
+    ("aid_comm_size", ctypes.c_int, [P, P, P]),
+    ("aid_index_shard_info", ctypes.c_int, [P, I64, P, P]),
+    ("aid_index_pack", ctypes.c_int, [P, I64, P, I64, P]),
+    ("aid_index_splice", ctypes.c_int, [P, I64, P, I32, I64, P, ctypes.c_uint32, P]),
     ("aid_index_save", ctypes.c_int, [P, ctypes.c_char_p]),
     ("aid_index_load", ctypes.c_int, [P, ctypes.c_char_p]),
     ("aid_query", ctypes.c_int, [P, P, P, I32, P, P]),
     ("aid_query_extracted", ctypes.c_int, [P, P, P]),
+    ("aid_query_pcm", ctypes.c_int, [P, P, P, I32, I32, P, P, P]),
     ("aid_exact_lane", ctypes.c_int, [P, P, P, I32, I32, I32, P, P, P]),
     ("aid_exact_windows", ctypes.c_int, [I64, I32, P, P, P]),
     ("aid_downmix", ctypes.c_int, [P, P, I64, P, P]),

@@ -10,13 +10,17 @@ whole catalog and can answer queries alone.
 
 RCCL has no all-gatherv: counts are all-gathered first, then every rank's
 postings padded to the largest count go through a single all-gather, and the
-padding is dropped on receive. Two implementations of that exchange:
-  * "native" (default on GPUs): aid_index_allgather in libaidfp over an RCCL
-    communicator the engine owns (aid_comm_create; rank 0's unique id is shared
-    with broadcast_object_list) -- device postings never leave the C ABI;
-  * "torch": `allgather_postings` with torch.distributed collectives. It is
-    device-agnostic, so it also runs under gloo on CPU tensors
-    (tests/test_catalog_dist.py).
+padding is dropped on receive. The exchange is three engine steps around two
+collectives -- aid_index_shard_info, aid_index_pack (shard -> padded device
+planes), aid_index_splice (gathered planes -> the index, failure-atomic) -- and
+two drivers run them:
+  * "native" (default on GPUs): aid_index_allgather in libaidfp runs both
+    all-gathers itself over an RCCL communicator the engine owns
+    (aid_comm_create; rank 0's unique id is shared with broadcast_object_list)
+    -- device postings never leave the C ABI;
+  * "torch": `exchange_postings` runs the same pack/splice around
+    torch.distributed collectives: RCCL on device tensors ("nccl"), or gloo on
+    host copies (several ranks sharing one GPU, tests/test_gpu_comm.py).
 """
 
 from __future__ import annotations
@@ -35,26 +39,40 @@ def shard(tracks, rank: int, world: int):
     return tracks[lo:hi]
 
 
-def allgather_postings(local, group=None):
-    """All-gather variable-length [n, 3] int32 posting blocks; returns [sum n, 3] in rank order."""
+def exchange_postings(eng, first: int = 0, group=None) -> int:
+    """Replace this rank's postings [first, n) by the union of every rank's, in rank order, through
+    torch.distributed collectives around aid_index_pack / aid_index_splice. Returns the postings held.
+
+    Under "nccl" the planes are all-gathered as device tensors; under gloo as host copies. `eng` needs
+    index_shard_info / index_pack / index_splice and device buffers from `eng.alloc_planes` when it has
+    one (tests use a host stand-in), else torch.cuda tensors."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    dev = local.device
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
-    counts = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(counts, n, group=group)
-    cnt = counts.cpu().tolist()
-    mx = max(cnt)
-    if mx == 0:
-        return local.new_zeros((0, 3))
-    send = local.new_zeros((mx, 3))
-    send[: local.shape[0]] = local
-    recv = local.new_empty((world * mx, 3))
-    dist.all_gather_into_tensor(recv, send, group=group)
-    recv = recv.view(world, mx, 3)
-    return torch.cat([recv[r, : cnt[r]] for r in range(world)], dim=0)
+    on_dev = dist.get_backend(group) == "nccl"
+    n, nt = eng.index_shard_info(first)
+    meta = torch.tensor([n, nt], dtype=torch.int64, device="cuda" if on_dev else "cpu")
+    allm = torch.empty(2 * world, dtype=torch.int64, device=meta.device)
+    dist.all_gather_into_tensor(allm, meta, group=group)
+    m = allm.view(world, 2).cpu().numpy()
+    counts, stride, tracks = m[:, 0].copy(), int(m[:, 0].max()), int(m[:, 1].max())
+    alloc = getattr(eng, "alloc_planes", None) or (lambda k: torch.empty(k, dtype=torch.int32, device="cuda"))
+    send = alloc(3 * stride)
+    if stride:
+        eng.index_pack(first, send.data_ptr(), stride)
+    if on_dev:
+        recv = alloc(3 * stride * world)
+        if stride:
+            dist.all_gather_into_tensor(recv, send, group=group)
+        torch.cuda.synchronize()  # the engine's stream reads what torch's stream gathered
+    else:
+        recv_h = torch.empty(3 * stride * world, dtype=torch.int32)
+        if stride:
+            dist.all_gather_into_tensor(recv_h, send.cpu(), group=group)
+        recv = alloc(3 * stride * world)
+        recv.copy_(recv_h)
+    return eng.index_splice(first, recv.data_ptr() if stride else 0, counts, stride, tracks)
 
 
 @dataclass
@@ -69,6 +87,7 @@ class IngestStats:
     exchange: str = "none"
     t_comm_init: float = 0.0
     t_synth: float = 0.0  # device time generating the synthetic PCM (inside t_extract's wall span)
+    rccl_nranks: int = 0  # ranks of the native RCCL communicator (ncclCommCount), 0 = none used
 
 
 def native_comm(eng, group=None) -> int:
@@ -120,36 +139,26 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     n_local = eng.index_stats()["postings"] - base
     total = n_local
     t_init = 0.0
+    nranks = 0
     if world > 1 and exchange == "native":
         ti = time.perf_counter()
         comm = native_comm(eng, group)
         t1 = time.perf_counter()
         t_init = t1 - ti
         try:
+            nranks = eng.comm_size(comm)[0]
             total = eng.index_allgather(comm, base) - base
         finally:
             eng.comm_destroy(comm)
         t2 = time.perf_counter()
     elif world > 1:
-        cols = torch.empty((3, max(n_local, 1)), dtype=torch.int32, device="cuda")
-        eng.index_export_device(cols[0].data_ptr(), cols[1].data_ptr(), cols[2].data_ptr(), base, n_local)
-        local = cols[:, :n_local].t().contiguous()
-        allp = allgather_postings(local, group)
+        total = exchange_postings(eng, base, group) - base
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        # replace this rank's postings by the gathered catalog (own shard included, rank order)
-        keep = eng.index_export(0, base) if base else None
-        eng.index_reset()
-        if keep is not None and len(keep):
-            k = torch.from_numpy(keep.astype(np.int32)).cuda().t().contiguous()
-            eng.index_add_postings(k[0].data_ptr(), k[1].data_ptr(), k[2].data_ptr(), k.shape[1])
-        g = allp.t().contiguous()
-        eng.index_add_postings(g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(), g.shape[1])
-        total = int(g.shape[1])
     else:
         t2 = t1
     eng.index_finalize()
     torch.cuda.synchronize()
     t3 = time.perf_counter()
     return IngestStats(len(mine), len(mine) * n / eng.sample_rate, n_local, total, t1 - t0 - t_init, t2 - t1,
-                       t3 - t2, exchange if world > 1 else "none", t_init, t_synth)
+                       t3 - t2, exchange if world > 1 else "none", t_init, t_synth, nranks)

@@ -1,0 +1,165 @@
+"""Concurrent readers at the boundary (SURVEY.md 8b "reentrant aid_query under shared lock").
+
+The reference runs one `olaf_c query` subprocess per request
+(audio-ident-service/app/audio/fingerprint.py:185-193), so concurrent searches query in
+parallel, while LMDB keeps a single writer (fingerprint.py:7-8, routers/ingest.py:49-52).
+Here the index lives in one GPU engine:
+
+  * `RWLock` -- index writers (store, delete, checkpoint) are exclusive; readers share.
+  * `QueryCoalescer` -- concurrent query requests are gathered into ONE engine call
+    (aid_query_pcm: K1-K3 + K5 over the whole batch). A dispatcher thread takes the first
+    waiting request, collects whatever else arrives within `window_s` (up to `max_batch`),
+    runs the batch under the read lock and resolves every request's future. Under load the
+    next batch accumulates while the current one runs on the GPU, so batching follows the
+    arrival rate and a lone request pays at most `window_s` extra.
+"""
+
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from concurrent.futures import Future
+from typing import Callable, Sequence
+
+logger = logging.getLogger(__name__)
+
+
+class RWLock:
+    """Writer-preferring reader/writer lock (a waiting writer blocks new readers)."""
+
+    def __init__(self):
+        self._cv = threading.Condition(threading.Lock())
+        self._readers = 0
+        self._writer = False
+        self._writers_waiting = 0
+
+    def acquire_read(self) -> None:
+        with self._cv:
+            while self._writer or self._writers_waiting:
+                self._cv.wait()
+            self._readers += 1
+
+    def release_read(self) -> None:
+        with self._cv:
+            self._readers -= 1
+            if self._readers == 0:
+                self._cv.notify_all()
+
+    def acquire_write(self) -> None:
+        with self._cv:
+            self._writers_waiting += 1
+            try:
+                while self._writer or self._readers:
+                    self._cv.wait()
+            finally:
+                self._writers_waiting -= 1
+            self._writer = True
+
+    def release_write(self) -> None:
+        with self._cv:
+            self._writer = False
+            self._cv.notify_all()
+
+    class _Guard:
+        def __init__(self, acq, rel):
+            self._acq, self._rel = acq, rel
+
+        def __enter__(self):
+            self._acq()
+            return self
+
+        def __exit__(self, *exc):
+            self._rel()
+
+    def read(self) -> "RWLock._Guard":
+        return RWLock._Guard(self.acquire_read, self.release_read)
+
+    def write(self) -> "RWLock._Guard":
+        return RWLock._Guard(self.acquire_write, self.release_write)
+
+
+_STOP = object()
+
+
+class QueryCoalescer:
+    """Gathers concurrent requests into batches for `run_batch(payloads) -> results` (same order)."""
+
+    def __init__(self, run_batch: Callable[[Sequence], Sequence], window_s: float = 0.0005, max_batch: int = 256):
+        self._run = run_batch
+        self.window_s = float(window_s)
+        self.max_batch = int(max_batch)
+        self._q: queue.SimpleQueue = queue.SimpleQueue()
+        self._thread: threading.Thread | None = None
+        self._start_lock = threading.Lock()
+        self.batches: list[int] = []  # sizes of the last batches run (bounded; tests and stats)
+
+    def submit(self, payload) -> Future:
+        fut: Future = Future()
+        self._ensure_thread()
+        self._q.put((payload, fut))
+        return fut
+
+    def __call__(self, payload):
+        return self.submit(payload).result()
+
+    def close(self) -> None:
+        with self._start_lock:
+            t, self._thread = self._thread, None
+        if t is not None:
+            self._q.put(_STOP)
+            t.join()
+
+    def _ensure_thread(self) -> None:
+        if self._thread is not None:
+            return
+        with self._start_lock:
+            if self._thread is None:
+                t = threading.Thread(target=self._loop, name="aidfp-query-coalescer", daemon=True)
+                t.start()
+                self._thread = t
+
+    def _loop(self) -> None:
+        while True:
+            first = self._q.get()
+            if first is _STOP:
+                return
+            batch = [first]
+            stop = False
+            deadline = time.monotonic() + self.window_s
+            while len(batch) < self.max_batch:
+                try:
+                    item = self._q.get_nowait()
+                except queue.Empty:
+                    left = deadline - time.monotonic()
+                    if left <= 0:
+                        break
+                    try:
+                        item = self._q.get(timeout=left)
+                    except queue.Empty:
+                        break
+                if item is _STOP:
+                    stop = True
+                    break
+                batch.append(item)
+            self._dispatch(batch)
+            if stop:
+                return
+
+    def _dispatch(self, batch) -> None:
+        self.batches.append(len(batch))
+        del self.batches[:-1024]
+        live = [(p, f) for p, f in batch if f.set_running_or_notify_cancel()]
+        if not live:
+            return
+        try:
+            results = self._run([p for p, _ in live])
+            if len(results) != len(live):
+                raise RuntimeError(f"batch runner returned {len(results)} results for {len(live)} requests")
+        except BaseException as exc:  # every request of the batch sees the failure
+            for _, f in live:
+                f.set_exception(exc)
+            return
+        for (_, f), r in zip(live, results):
+            f.set_result(r)

@@ -76,6 +76,13 @@ class Engine:
     def __exit__(self, *exc):
         self.close()
 
+    FORCE = {"k5_path": L.AID_FORCE_K5_PATH, "k5_parts": L.AID_FORCE_K5_PARTS, "k5_batch": L.AID_FORCE_K5_BATCH,
+             "k2_strips_x100": L.AID_FORCE_K2_STRIPS_X100, "k4_build": L.AID_FORCE_K4_BUILD}
+
+    def force(self, what: str, value: int) -> None:
+        """Test hook (aid_engine_force): pin one of the engine's own code paths, e.g. force("k5_path", 2)."""
+        check(self._lib.aid_engine_force(self._h, self.FORCE[what], int(value)))
+
     # -- sizes --
     def num_frames(self, n: int) -> int:
         return int(self._lib.aid_num_frames(self._h, int(n)))
@@ -153,11 +160,13 @@ class Engine:
         return out[:F]
 
     def synth(self, dst_ptr: int, tracks, starts, n: int, noise_a: int = 0, salt: int = 0,
-              stream: int | None = None) -> None:
+              stream: int | None = None, fmax_hz: int = 8000) -> None:
+        """aidfp.synth's PCM into device memory [n_clips][n] (partials in [100, fmax_hz) Hz)."""
         tr = np.ascontiguousarray(tracks, dtype=np.uint32)
         st = np.ascontiguousarray(starts, dtype=np.int64)
-        check(self._lib.aid_synth(self._h, ctypes.c_void_p(dst_ptr), _p(tr), _p(st), len(tr), int(n), int(noise_a),
-                                  int(salt) & 0xFFFFFFFF, ctypes.c_void_p(stream) if stream else None))
+        check(self._lib.aid_synth_band(self._h, ctypes.c_void_p(dst_ptr), _p(tr), _p(st), len(tr), int(n),
+                                       int(noise_a), int(salt) & 0xFFFFFFFF, int(fmax_hz),
+                                       ctypes.c_void_p(stream) if stream else None))
 
     # -- index + match (FPSPEC 7) --
     def index_reset(self) -> None:
@@ -256,6 +265,31 @@ class Engine:
         check(self._lib.aid_index_allgather(self._h, ctypes.c_void_p(comm), int(first), ctypes.byref(n)))
         return int(n.value)
 
+    def comm_size(self, comm: int) -> tuple[int, int]:
+        """(ranks, this rank) as the RCCL communicator sees them (ncclCommCount / ncclCommUserRank)."""
+        w, r = ctypes.c_int32(), ctypes.c_int32()
+        check(self._lib.aid_comm_size(ctypes.c_void_p(comm), ctypes.byref(w), ctypes.byref(r)))
+        return int(w.value), int(r.value)
+
+    def index_shard_info(self, first: int = 0) -> tuple[int, int]:
+        """(postings in [first, n), n_tracks): what this rank contributes to an index exchange."""
+        n, nt = ctypes.c_int64(), ctypes.c_uint32()
+        check(self._lib.aid_index_shard_info(self._h, int(first), ctypes.byref(n), ctypes.byref(nt)))
+        return int(n.value), int(nt.value)
+
+    def index_pack(self, first: int, planes_ptr: int, stride: int, stream: int | None = None) -> None:
+        """Copy this rank's shard [first, n) into device planes [3][stride] (hash, track, t; zero padded)."""
+        check(self._lib.aid_index_pack(self._h, int(first), ctypes.c_void_p(planes_ptr), int(stride),
+                                       ctypes.c_void_p(stream) if stream else None))
+
+    def index_splice(self, first: int, recv_ptr: int, counts, stride: int, n_tracks: int,
+                     stream: int | None = None) -> int:
+        """Replace [first, n) by the gathered shards (device recv [world][3][stride]); failure-atomic."""
+        c = np.ascontiguousarray(counts, dtype=np.int64)
+        check(self._lib.aid_index_splice(self._h, int(first), ctypes.c_void_p(recv_ptr), len(c), int(stride), _p(c),
+                                         int(n_tracks), ctypes.c_void_p(stream) if stream else None))
+        return self.index_stats()["postings"]
+
     def index_export(self, first: int = 0, count: int | None = None) -> np.ndarray:
         """Host copy of stored postings [first, first+count) as [n, 3] uint32 (hash, track, t)."""
         total = self.index_stats()["postings"]
@@ -300,6 +334,22 @@ class Engine:
         rows = (AidMatchRow * (nq * self.max_results))()
         nrows = np.zeros(nq, dtype=np.int32)
         check(self._lib.aid_query_extracted(self._h, ctypes.addressof(rows), _p(nrows)))
+        return self._rows(rows, nrows, nq)
+
+    def query_pcm(self, clips: Sequence[np.ndarray]) -> list[np.ndarray]:
+        """Extract + match host clips in one engine call (aid_query_pcm; thread-safe as a unit)."""
+        arrs = [np.ascontiguousarray(c, dtype=np.float32).ravel() for c in clips]
+        nq = len(arrs)
+        if nq == 0:
+            return []
+        offsets = np.zeros(nq + 1, dtype=np.int64)
+        offsets[1:] = np.cumsum([len(a) for a in arrs])
+        pcm = np.concatenate(arrs) if offsets[-1] else np.zeros(1, dtype=np.float32)
+        rows = (AidMatchRow * (nq * self.max_results))()
+        nrows = np.zeros(nq, dtype=np.int32)
+        check(self._lib.aid_query_pcm(self._h, _p(pcm), _p(offsets), nq, AID_PCM_HOST, ctypes.addressof(rows),
+                                      _p(nrows), None))
+        self.n_clips = nq
         return self._rows(rows, nrows, nq)
 
     # -- batched exact lane --

@@ -20,9 +20,12 @@ Error contract (reference :102-155, :173-219, :234-270):
   * a recoverable engine error (bad input, unknown track on delete) -> False / []
     (logged), like a non-zero olaf_c exit code;
   * anything unexpected -> OlafError.
-Index writes are serialised by one lock (the reference's LMDB single-writer
-rule, :7-8); engine calls run in a worker thread (ctypes releases the GIL), so
-the event loop is never blocked.
+Concurrency (aidfp.concurrency): index writes take a reader/writer lock exclusively
+(the reference's LMDB single-writer rule, :7-8); queries share it. Concurrent
+olaf_query calls -- the reference runs one `olaf_c query` process each (:185-193)
+-- are coalesced into one engine call (aid_query_pcm) by a dispatcher thread, and
+the coroutine awaits its own future, so the event loop is never blocked. Writes run
+in a worker thread (ctypes releases the GIL).
 """
 
 from __future__ import annotations
@@ -31,11 +34,14 @@ import asyncio
 import logging
 import os
 import threading
+import time
 import uuid
 from dataclasses import dataclass
 from pathlib import Path
 
 import numpy as np
+
+from .concurrency import QueryCoalescer, RWLock
 
 logger = logging.getLogger(__name__)
 
@@ -99,15 +105,21 @@ class FingerprintService:
     """One GPU engine + the persisted index of the OLAF_DB directory (aidfp.store: snapshot +
     write-ahead journal, so a store or delete writes O(track) bytes, not the whole index)."""
 
-    def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20):
+    def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20,
+                 coalesce_window_s: float = 0.0005, max_batch: int = 256):
         self.db_dir = Path(db_dir) if db_dir is not None else db_path()
         self.device = device
-        self._lock = threading.Lock()
+        self._rw = RWLock()  # index writers exclusive, queries shared
+        self._init_lock = threading.Lock()  # first-use engine creation + index load
+        self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch)
+        self._ckpt_retry_at = 0.0  # monotonic time before which a failed auto-checkpoint is not retried
         self._engine = None
         self._store = None
         self._ids: dict[str, int] = {}  # uuid string -> engine track id
         self._names: dict[int, str] = {}
         self._next = 0
+        # persist = False: stores and deletes skip the journal and the automatic checkpoints (bulk
+        # ingest); the catalog on disk is still loaded first, and checkpoint() writes everything
         self.persist = True
         self.checkpoint_min_bytes = checkpoint_min_bytes
 
@@ -117,6 +129,12 @@ class FingerprintService:
         keeps it only once the saved index has been loaded completely: a failed load destroys
         the engine and raises OlafError, so nothing is ever written over a catalog that was not
         read (the next call retries the load)."""
+        if self._engine is not None:
+            return self._engine
+        with self._init_lock:
+            return self._eng_locked()
+
+    def _eng_locked(self):
         if self._engine is None:
             from ._lib import EngineError, EngineUnavailable
             from .engine import Engine
@@ -130,17 +148,13 @@ class FingerprintService:
             ids: dict[str, int] = {}
             names: dict[int, str] = {}
             try:
-                if self.persist:
-                    ids, nxt, entries = store.load(eng)
-                    names = {v: k for k, v in ids.items()}
-                    for op, track, name, recs in entries:  # replay the journal in order
-                        if op == OP_STORE:
-                            self._apply_store(eng, ids, names, track, name, recs)
-                        else:
-                            self._apply_delete(eng, ids, names, track, name)
-                else:
-                    nxt = 0
-                    store.loaded = True
+                ids, nxt, entries = store.load(eng)
+                names = {v: k for k, v in ids.items()}
+                for op, track, name, recs in entries:  # replay the journal in order
+                    if op == OP_STORE:
+                        self._apply_store(eng, ids, names, track, name, recs)
+                    else:
+                        self._apply_delete(eng, ids, names, track, name)
             except (EngineError, StoreCorrupt, OSError) as exc:
                 eng.close()
                 raise OlafError(f"cannot load the fingerprint index in {self.db_dir}: {exc}") from exc
@@ -181,11 +195,20 @@ class FingerprintService:
         names.pop(track, None)
 
     def _maybe_checkpoint(self) -> None:
-        if self.persist and self._store.should_checkpoint():
-            try:
-                self._store.checkpoint(self._engine, dict(self._ids), self._next)
-            except OSError:  # the journal still holds every operation: nothing is lost
-                logger.exception("aidfp index checkpoint failed (journal kept)")
+        """Automatic checkpoint after a write. The operation is already journaled (fsynced) and applied,
+        so a failed checkpoint (full disk, permissions, device error in the compaction) is logged and
+        the journal kept -- the caller still gets True -- and retried no sooner than 60 s later."""
+        from ._lib import EngineError
+
+        if not (self.persist and self._store.should_checkpoint()) or time.monotonic() < self._ckpt_retry_at:
+            return
+        try:
+            self._store.checkpoint(self._engine, dict(self._ids), self._next)
+        except (OSError, EngineError):  # the journal still holds every operation: nothing is lost
+            logger.exception("aidfp index checkpoint failed (journal kept)")
+            self._ckpt_retry_at = time.monotonic() + 60.0
+            for tmp in self.db_dir.glob("*.tmp"):
+                tmp.unlink(missing_ok=True)
 
     @staticmethod
     def _pcm(buf: bytes) -> np.ndarray:
@@ -195,7 +218,7 @@ class FingerprintService:
     def index_track(self, pcm: bytes, name: str) -> bool:
         from ._lib import EngineError
 
-        with self._lock:
+        with self._rw.write():
             eng = self._eng()
             try:
                 recs = eng.extract_host([self._pcm(pcm)])[0]
@@ -229,34 +252,44 @@ class FingerprintService:
             self._names.pop(old, None)
             eng.index_remove(old)
 
+    def submit_query(self, pcm: bytes):
+        """Queue one query for the coalescer; returns a concurrent.futures.Future of list[OlafMatch]."""
+        return self._coalescer.submit(pcm)
+
     def query(self, pcm: bytes) -> list[OlafMatch]:
+        return self._coalescer(pcm)
+
+    def _query_batch(self, pcms: list[bytes]) -> list[list[OlafMatch]]:
+        """One engine call for every query the coalescer gathered (under the shared lock)."""
         from ._lib import EngineError
 
-        with self._lock:
+        with self._rw.read():
             eng = self._eng()
             try:
-                eng.extract_host([self._pcm(pcm)])
-                rows = eng.query_extracted()[0]
+                rows = eng.query_pcm([self._pcm(p) for p in pcms])
             except EngineError as exc:
-                logger.error("aidfp query failed: %s", exc)
-                return []
+                logger.error("aidfp query batch of %d failed: %s", len(pcms), exc)
+                return [[] for _ in pcms]
             sec = eng.hop / eng.sample_rate
-            out = []
-            for count, track, d, tq0, tq1 in rows.tolist():
-                name = self._names.get(int(track))
-                if name is None:
-                    continue
-                out.append(OlafMatch(int(count), tq0 * sec, tq1 * sec, name, int(track), (tq0 + d) * sec,
-                                     (tq1 + d) * sec))
-            out.sort(key=lambda m: m.match_count, reverse=True)
-            return out
+            outs = []
+            for r in rows:
+                out = []
+                for count, track, d, tq0, tq1 in r.tolist():
+                    name = self._names.get(int(track))
+                    if name is None:
+                        continue
+                    out.append(OlafMatch(int(count), tq0 * sec, tq1 * sec, name, int(track), (tq0 + d) * sec,
+                                         (tq1 + d) * sec))
+                out.sort(key=lambda m: m.match_count, reverse=True)
+                outs.append(out)
+            return outs
 
     def exact_batch(self, clips: list[bytes], max_results: int) -> list[list]:
         """Batched exact lane over the engine (aid_exact_lane); ranked ScoredCandidate lists."""
         from ._lib import EngineError
         from .exact import candidates_from_rows
 
-        with self._lock:
+        with self._rw.read():
             eng = self._eng()
             pcms = [self._pcm(c) for c in clips]
             try:
@@ -270,7 +303,7 @@ class FingerprintService:
     def delete_track(self, name: str) -> bool:
         from ._lib import EngineError
 
-        with self._lock:
+        with self._rw.write():
             eng = self._eng()
             tid = self._ids.get(name)
             if tid is None:
@@ -293,14 +326,15 @@ class FingerprintService:
             return True
 
     def checkpoint(self) -> None:
-        """Fold the journal into a new snapshot now (compacting removed tracks' postings)."""
-        with self._lock:
+        """Write a snapshot of the whole index now (compacting removed tracks' postings) and start an
+        empty journal. Always writes, also with persist = False: that is how a bulk ingest commits."""
+        with self._rw.write():
             self._eng()
-            if self.persist:
-                self._store.checkpoint(self._engine, dict(self._ids), self._next)
+            self._store.checkpoint(self._engine, dict(self._ids), self._next)
 
     def close(self) -> None:
-        with self._lock:
+        self._coalescer.close()
+        with self._rw.write():
             if self._engine is not None:
                 self._engine.close()
                 self._engine = None
@@ -347,7 +381,8 @@ async def olaf_query(pcm_16k_f32le: bytes) -> list[OlafMatch]:
     if not pcm_16k_f32le:
         return []
     try:
-        return await _run(get_service().query, pcm_16k_f32le)
+        # coalesced with the other queries in flight (one engine call per batch); no worker thread waits
+        return await asyncio.wrap_future(get_service().submit_query(pcm_16k_f32le))
     except OlafError:
         raise
     except Exception as exc:

@@ -13,7 +13,7 @@ at ``:602-606``) and query offsets drawn uniformly (``:481-483``).
 Signal of track ``tr`` at absolute sample ``i``:
   * a new "note" every ``sr // 4`` samples (250 ms), ``j = i // note_len``;
   * 8 partials ``p``: phase increment ``inc = inc_min + (R(tr,p,j) * inc_rng) >> 32``
-    (100 Hz .. 8 kHz), amplitude ``A = 983 + R(tr,p+8,j) % 2949`` (0.03 .. 0.12 FS),
+    (100 Hz .. 8 kHz; ``fmax_hz`` widens the band, e.g. 20 kHz for the full-band workload), amplitude ``A = 983 + R(tr,p+8,j) % 2949`` (0.03 .. 0.12 FS),
     phase ``ph = R(tr,p+16,j) + inc * (i - j*note_len)`` (mod 2^32),
     value ``(A * SIN[ph >> 20]) >> 15`` with ``SIN[k] = round(32767 sin(2 pi k / 4096))``;
   * base noise ``R(tr,24,i) % 1137 - 568`` (about -40 dBFS rms);
@@ -56,9 +56,9 @@ def rnd(track, stream, idx) -> np.ndarray:
         return _mix(b + np.asarray(idx, dtype=np.uint64).astype(np.uint32))
 
 
-def inc_params(sr: int) -> tuple[int, int]:
+def inc_params(sr: int, fmax_hz: int = 8000) -> tuple[int, int]:
     inc_min = int(np.floor(100.0 / sr * 4294967296.0))
-    inc_rng = int(np.floor(7900.0 / sr * 4294967296.0))
+    inc_rng = int(np.floor((fmax_hz - 100) / sr * 4294967296.0))
     return inc_min, inc_rng
 
 
@@ -70,12 +70,13 @@ def noise_halfwidth(snr_db: float | None) -> int:
     return int(round(rms * np.sqrt(3.0)))
 
 
-def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt: int = 0) -> np.ndarray:
+def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt: int = 0,
+                fmax_hz: int = 8000) -> np.ndarray:
     """int32 array of int16-range samples of track ``track`` at absolute samples start..start+n."""
     if n <= 0:
         return np.zeros(0, dtype=np.int32)
     note_len = sr // 4
-    inc_min, inc_rng = inc_params(sr)
+    inc_min, inc_rng = inc_params(sr, fmax_hz)
     i = np.arange(start, start + n, dtype=np.int64)
     j = i // note_len
     rel = (i - j * note_len).astype(np.uint64)
@@ -93,9 +94,10 @@ def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt:
     return np.clip(acc, -32768, 32767).astype(np.int32)
 
 
-def synth(track: int, start: int, n: int, sr: int, snr_db: float | None = None, salt: int = 0) -> np.ndarray:
+def synth(track: int, start: int, n: int, sr: int, snr_db: float | None = None, salt: int = 0,
+          fmax_hz: int = 8000) -> np.ndarray:
     """float32 PCM in [-1, 1): int16 samples / 32768 (exact)."""
-    q = synth_int16(track, start, n, sr, noise_halfwidth(snr_db), salt)
+    q = synth_int16(track, start, n, sr, noise_halfwidth(snr_db), salt, fmax_hz)
     return (q.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
 
 

@@ -47,9 +47,6 @@ __device__ __forceinline__ float2 cmul(float2 x, float2 w) {
 // in aid_engine_create: T16[2] = (c, -c), T16[6] = (-c, -c), T16[4] = (e, -1)). Each returns exactly
 // cmul(x, w): x.im * w.im is -(x.im * c) (or x.im * e, -x.im) bit for bit, so one product serves both
 // components -- 3 VALU instead of 4.
-#ifndef AID_DFT16_SYM
-#define AID_DFT16_SYM 1
-#endif
 __device__ __forceinline__ float2 cmul_w2(float2 x, float c) {  // w = (c, -c)
     const float t = x.y * c;  // -(x.im * w.im) and x.im * w.re
     return make_float2(__builtin_fmaf(x.x, c, t), __builtin_fmaf(x.x, -c, t));
@@ -71,85 +68,28 @@ __device__ __forceinline__ void dft4(float2 &a, float2 &b, float2 &c, float2 &d)
     d = make_float2(t1.x - t3.y, t1.y + t3.x);
 }
 
-// AID_PK_DFT4=1: the DFT4 butterflies as packed FP32 (v_pk_add_f32 on (re, im) register pairs; the -i
-// rotations through op_sel/neg modifiers). Same IEEE binary32 additions as dft4() above, bit for bit:
-// 8 VALU instead of 16 per DFT4 (a packed add issues at ~1.1-1.2x the pair rate of two scalar adds,
-// probes/pk_add_probe: so the gain is issue slots and ~10 % of the butterflies' VALU time).
-#ifndef AID_PK_DFT4
-#define AID_PK_DFT4 0
-#endif
-typedef float aid_pk2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ aid_pk2 pk_of(float2 a) { return (aid_pk2){a.x, a.y}; }
-__device__ __forceinline__ float2 f2_of(aid_pk2 a) { return make_float2(a.x, a.y); }
-__device__ __forceinline__ aid_pk2 pk_add(aid_pk2 a, aid_pk2 b) {
-    aid_pk2 r;
-    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ aid_pk2 pk_sub(aid_pk2 a, aid_pk2 b) {
-    aid_pk2 r;
-    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ aid_pk2 pk_add_mi(aid_pk2 a, aid_pk2 b) {  // (a.re + b.im, a.im - b.re)
-    aid_pk2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ aid_pk2 pk_add_pi(aid_pk2 a, aid_pk2 b) {  // (a.re - b.im, a.im + b.re)
-    aid_pk2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ aid_pk2 pk_mul(aid_pk2 a, aid_pk2 b) {
-    aid_pk2 r;
-    asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ void dft4_pk(float2 &a, float2 &b, float2 &c, float2 &d) {
-    const aid_pk2 x0 = pk_of(a), x1 = pk_of(b), x2 = pk_of(c), x3 = pk_of(d);
-    const aid_pk2 t0 = pk_add(x0, x2), t1 = pk_sub(x0, x2), t2 = pk_add(x1, x3), t3 = pk_sub(x1, x3);
-    a = f2_of(pk_add(t0, t2));
-    c = f2_of(pk_sub(t0, t2));
-    b = f2_of(pk_add_mi(t1, t3));
-    d = f2_of(pk_add_pi(t1, t3));
-}
-
 // FPSPEC 3 DFT16: v[16] in natural input order -> out[c + 4d] in v (natural output order).
 // t16 holds W16^1, W16^2, W16^3, W16^4 (unused), W16^6, W16^9 at indices 1,2,3,4,6,9.
-// b0 > 0: the caller already ran the first-round DFT4s of b < b0 (staged E1 reads in K1)
-__device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10], const int b0 = 0) {
+__device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10]) {
     // s[b][c] lives in v[b + 4c] after the first DFT4 over (b, b+4, b+8, b+12)
 #pragma unroll
-    for (int b = b0; b < 4; ++b) {
-        if (AID_PK_DFT4) dft4_pk(v[b], v[b + 4], v[b + 8], v[b + 12]);
-        else dft4(v[b], v[b + 4], v[b + 8], v[b + 12]);
-    }
+    for (int b = 0; b < 4; ++b) dft4(v[b], v[b + 4], v[b + 8], v[b + 12]);
     // twiddles W16^{b*c}, b,c in 1..3
     v[1 + 4 * 1] = cmul(v[1 + 4 * 1], t16[1]);
     v[1 + 4 * 3] = cmul(v[1 + 4 * 3], t16[3]);
     v[3 + 4 * 1] = cmul(v[3 + 4 * 1], t16[3]);
     v[3 + 4 * 3] = cmul(v[3 + 4 * 3], t16[9]);
-#if AID_DFT16_SYM
     v[1 + 4 * 2] = cmul_w2(v[1 + 4 * 2], t16[2].x);
     v[2 + 4 * 1] = cmul_w2(v[2 + 4 * 1], t16[2].x);
     v[2 + 4 * 2] = cmul_w4(v[2 + 4 * 2], t16[4].x);
     v[2 + 4 * 3] = cmul_w6(v[2 + 4 * 3], t16[6].x);
     v[3 + 4 * 2] = cmul_w6(v[3 + 4 * 2], t16[6].x);
-#else
-    v[1 + 4 * 2] = cmul(v[1 + 4 * 2], t16[2]);
-    v[2 + 4 * 1] = cmul(v[2 + 4 * 1], t16[2]);
-    v[2 + 4 * 2] = cmul(v[2 + 4 * 2], t16[4]);
-    v[2 + 4 * 3] = cmul(v[2 + 4 * 3], t16[6]);
-    v[3 + 4 * 2] = cmul(v[3 + 4 * 2], t16[6]);
-#endif
     // second DFT4 over b for each c: inputs v[0+4c..3+4c], outputs out[c + 4d]
     float2 o[16];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         float2 a0 = v[0 + 4 * c], a1 = v[1 + 4 * c], a2 = v[2 + 4 * c], a3 = v[3 + 4 * c];
-        if (AID_PK_DFT4) dft4_pk(a0, a1, a2, a3);
-        else dft4(a0, a1, a2, a3);
+        dft4(a0, a1, a2, a3);
         o[c + 0] = a0;
         o[c + 4] = a1;
         o[c + 8] = a2;
@@ -159,20 +99,12 @@ __device__ __forceinline__ void dft16(float2 (&v)[16], const float2 (&t16)[10], 
     for (int i = 0; i < 16; ++i) v[i] = o[i];
 }
 
-// compiler + hardware ordering point for wave-private LDS exchanges
 // Orders a wave's own LDS exchange (write -> read by other lanes of the SAME wave). A wave's
 // LDS instructions are executed in issue order (LLVM AMDGPU memory model: LDS accesses of one
-// wavefront stay in order), so only the compiler must be kept from moving accesses across; the
-// s_waitcnt form (AID_K1_LDS_WAIT=1) additionally stalls the wave for a full round trip.
-#ifndef AID_K1_LDS_WAIT
-#define AID_K1_LDS_WAIT 0
-#endif
+// wavefront stay in order), so only the compiler must be kept from moving accesses across
+// (an s_waitcnt here measured equal: the wait is not the cost).
 __device__ __forceinline__ void wave_lds_sync() {
-#if AID_K1_LDS_WAIT
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
     asm volatile("" ::: "memory");
-#endif
 }
 
 }  // namespace aid

@@ -24,17 +24,15 @@
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, bool keep_power, float *dummy, hipStream_t s);
+                       uint32_t *hot, float thr, bool keep_power, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
-                      const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink, uint32_t *cold_cnt,
-                      hipStream_t s);
-bool peak_pick_counts_cold();
+                      const uint32_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s);
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
-                      uint64_t *k2_cold_host, uint32_t k2_waves, hipStream_t s);
+                      uint64_t *k2_cold_host, uint32_t k2_waves, bool one_chunk_each, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
-                  int noise_a, uint32_t salt, const int16_t *sin_tab, hipStream_t s);
+                  int noise_a, uint32_t salt, int fmax_hz, const int16_t *sin_tab, hipStream_t s);
 int64_t resample_lds_floats(int up, int down, int J);
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
                      const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s);
@@ -139,13 +137,10 @@ struct aid_engine {
     DevBuf<float> power;
     DevBuf<uint64_t> mask;
     DevBuf<uint32_t> hotw;  // K1 -> K2: per power row, bit b = 64-bin block b has a value > thr
-    DevBuf<float> k1_dummy;  // K1's sink for cold-block stores: kK1DummyRows x 2048 floats
-    DevBuf<float> k2_zero;   // K2: a 1024-float zero row (cold-block loads)
-    DevBuf<uint64_t> k2_sink;  // K2: mask-store sink, kK2SinkBlocks x 256 words
     DevBuf<uint32_t> k2_cold;  // K2: strip-cold wave counters (64), summed and reset by K3
     uint64_t *h_cold = nullptr;      // pinned, host-mapped: K3 stores (cold waves | waves << 32) of the last K2 here
     uint64_t *h_cold_dev = nullptr;  // its device address
-    double k2_slots_x = 0.0;         // AIDFP_K2_SLOTS_X: fixed strips per slot; 0 = adaptive (extract_locked)
+    double k2_slots_x = 0.0;         // aid_engine_force K2_STRIPS: fixed strips per slot; 0 = adaptive (extract_locked)
     DevBuf<ClipDesc> desc;
     DevBuf<int64_t> chunk_counts;
     DevBuf<uint64_t> records;
@@ -164,7 +159,7 @@ struct aid_engine {
     DevBuf<uint32_t> srt_k0, srt_k1;  // K4 sort build: key double buffer
     DevBuf<uint64_t> srt_v;           // K4 sort build: the value buffer idx_post pairs with
     DevBuf<uint8_t> srt_tmp;          // K4 sort build: radix-sort temporary storage
-    int k4_mode = 1;                  // AIDFP_K4: 1 = sort build (default), 0 = atomic counting sort
+    int k4_mode = 1;                  // aid_engine_force K4_BUILD: 1 = sort build (default), 0 = atomic counting sort
     bool index_built = false, index_dirty = true;
     int64_t n_indexed = 0;
     int64_t n_buckets_used = 0;
@@ -213,10 +208,11 @@ struct aid_engine {
     int64_t total_frames = 0, total_strips = 0, total_chunks = 0, total_records = 0;
     int64_t k2_slots = 1;  // resident K2 workgroups on the device (CUs x blocks per CU)
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
-    int k5_path = 0;       // AIDFP_K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
-    int k5_parts = 0;      // AIDFP_K5_PARTS: K5a key partitions per query (0 = by vote count)
+    int k5_path = 0;       // aid_engine_force K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
+    int k5_parts = 0;      // aid_engine_force K5_PARTS: K5a key partitions per query (0 = by vote count)
+    bool k5_spec_ok = true;  // the previous query batch's heaviest query fitted the LDS path (speculation gate)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
-    size_t k5_batch = 2048;        // global-path queries per launch (AIDFP_K5_BATCH)
+    size_t k5_batch = 2048;        // global-path queries per launch
     hipStream_t last_stream = nullptr;
     bool have_result = false;
 
@@ -350,16 +346,6 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     e->device = dev;
     e->k2_slots = (int64_t)prop.multiProcessorCount * peak_pick_blocks_per_cu();
     e->k1_slots = (int64_t)prop.multiProcessorCount * kStftWaves;
-    if (const char *kx = std::getenv("AIDFP_K2_SLOTS_X"))  // fixed K2 strips per slot (0 = adaptive, the default)
-        e->k2_slots_x = std::max(0.0, std::atof(kx));
-    if (const char *kp = std::getenv("AIDFP_K5_PARTS")) {  // 1, 2 or 4 (0 = by vote count)
-        const int v = std::atoi(kp);
-        e->k5_parts = v >= 4 ? 4 : v >= 2 ? 2 : v >= 1 ? 1 : 0;
-    }
-    if (const char *kb = std::getenv("AIDFP_K5_BATCH")) e->k5_batch = std::max(1, std::atoi(kb));
-    if (const char *k4 = std::getenv("AIDFP_K4")) e->k4_mode = std::strcmp(k4, "atomic") == 0 ? 0 : 1;
-    if (const char *kp = std::getenv("AIDFP_K5_PATH"))
-        e->k5_path = std::strcmp(kp, "lds") == 0 ? 1 : std::strcmp(kp, "global") == 0 ? 2 : 0;
     // blocking stream: ordered against the legacy default stream (torch's default), so device
     // buffers the caller filled there without a stream handle are complete before NULL-stream calls
     hipError_t he = hipStreamCreateWithFlags(&e->own_stream, hipStreamDefault);
@@ -369,7 +355,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     }
     Tables *h = new Tables();
     build_tables(*h);
-    // K1 (AID_K1_T2HALF) derives the real split's mirror twiddle T2K[1024-k] as (-re, im) of T2K[k]
+    // K1 derives the real split's mirror twiddle T2K[1024-k] as (-re, im) of T2K[k]
     for (int k = 1; k < 512; ++k)
         if (!(h->t2k[1024 - k].x == -h->t2k[k].x && h->t2k[1024 - k].y == h->t2k[k].y)) {
             delete h;
@@ -377,7 +363,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
             delete e;
             return fail(AID_ERR_DEVICE, "twiddle table lacks the mirror symmetry K1 relies on");
         }
-    // K1's DFT16 (AID_DFT16_SYM, aidfp_device.h) shares one product in the cmuls by T16[2], T16[4], T16[6]
+    // K1's DFT16 (aidfp_device.h) shares one product in the cmuls by T16[2], T16[4], T16[6]
     {
         const float2 w2 = h->t16[2], w4 = h->t16[4], w6 = h->t16[6];
         if (!(w2.y == -w2.x && w6.x == w6.y && w6.x == -w2.x && w4.y == -1.0f)) {
@@ -414,9 +400,6 @@ void aid_engine_destroy(aid_engine *e) {
     for (auto ev : e->pool) (void)hipEventDestroy(ev);
     e->pcm_stage.release();
     e->power.release();
-    e->k1_dummy.release();
-    e->k2_zero.release();
-    e->k2_sink.release();
     e->k2_cold.release();
     if (e->h_cold) (void)hipHostFree(e->h_cold);
     e->mask.release();
@@ -489,6 +472,37 @@ int aid_engine_config(const aid_engine *e, aid_config *out) {
     return AID_OK;
 }
 
+int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    switch (what) {
+        case AID_FORCE_K5_PATH:
+            if (value < 0 || value > 2) return fail(AID_ERR_INVALID, "K5_PATH: 0 auto, 1 LDS first, 2 global");
+            e->k5_path = value;
+            return AID_OK;
+        case AID_FORCE_K5_PARTS:
+            if (value != 0 && value != 1 && value != 2 && value != 4) return fail(AID_ERR_INVALID, "K5_PARTS: 0, 1, 2 or 4");
+            e->k5_parts = value;
+            return AID_OK;
+        case AID_FORCE_K5_BATCH:
+            if (value < 0) return fail(AID_ERR_INVALID, "K5_BATCH must be >= 0");
+            e->k5_batch = value ? (size_t)value : 2048;
+            return AID_OK;
+        case AID_FORCE_K2_STRIPS_X100:
+            if (value < 0) return fail(AID_ERR_INVALID, "K2_STRIPS_X100 must be >= 0");
+            e->k2_slots_x = value / 100.0;
+            e->desc_dev_for_key = nullptr;  // strip bases change: rebuild the descriptors
+            return AID_OK;
+        case AID_FORCE_K4_BUILD:
+            if (value < 0 || value > 2) return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 sort, 2 atomic");
+            e->k4_mode = value == 2 ? 0 : 1;
+            e->index_dirty = true;
+            return AID_OK;
+        default:
+            return fail(AID_ERR_INVALID, "aid_engine_force: unknown path id");
+    }
+}
+
 int64_t aid_num_frames(const aid_engine *e, int64_t n) { return e ? num_frames(n, e->cfg.hop) : 0; }
 
 int64_t aid_hash_capacity(const aid_engine *e, int64_t n) { return e ? hash_capacity(num_frames(n, e->cfg.hop)) : 0; }
@@ -536,8 +550,12 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     e->clip_frames.assign(n_clips, 0);
     int64_t frames = 0, strips = 0, chunks = 0, recs = 0, staged = 0, kstrips = 0;
     bool empty_clip = false;  // a clip without frames gets no count from K3: zero the counts first
+    // K3 (landmarks.hip): a clip of several chunks needs the COUNT pass for its chunk bases; when every clip is
+    // exactly one chunk, a workgroup's clip is its chunk index. Neither follows from the totals alone: a clip
+    // too short for a frame has no chunk, so [short, two-chunk] also has as many chunks as clips
+    bool multi_chunk = false, one_chunk_each = n_clips > 0;
     for (int c = 0; c < n_clips; ++c) e->clip_frames[c] = num_frames(offsets[c + 1] - offsets[c], hop);
-    // K2 strips per resident workgroup slot. Strip-cold K2 waves exit (peaks.hip AID_K2_WCOLD_EXIT) and their
+    // K2 strips per resident workgroup slot. Strip-cold K2 waves exit (peaks.hip) and their
     // registers admit more workgroups per CU (LDS allows 7 instead of the 4 of an all-hot CU): with the
     // fraction c of cold waves counted in earlier calls (K3 stores it in pinned memory; read without a sync,
     // so it lags a few calls), the strips are made shorter and more numerous, 0.75 / (1 - c) per slot,
@@ -574,6 +592,9 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         e->clip_base[c] = recs;
         e->clip_frames[c] = F;
         empty_clip |= F == 0;
+        const int64_t nck = (F + kHashChunk - 1) / kHashChunk;
+        multi_chunk |= nck > 1;
+        one_chunk_each &= nck == 1;
         frames += F;
         strips += (F + strip_len - 1) / strip_len;
         chunks += (F + kHashChunk - 1) / kHashChunk;
@@ -584,17 +605,11 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     HIP_TRY(e->power.reserve((size_t)frames * kBins));
     HIP_TRY(e->mask.reserve((size_t)frames * kMaskWords));
     HIP_TRY(e->hotw.reserve((size_t)frames + 1));
-    HIP_TRY(e->k1_dummy.reserve((size_t)kK1DummyRows * 2048));
-    if (!e->k2_zero.p) {
-        HIP_TRY(e->k2_zero.reserve(kBins));
-        HIP_TRY(hipMemsetAsync(e->k2_zero.p, 0, kBins * sizeof(float), s));
-    }
-    HIP_TRY(e->k2_sink.reserve((size_t)kK2SinkBlocks * 256));
     if (!e->k2_cold.p) {
         HIP_TRY(e->k2_cold.reserve(64));
         HIP_TRY(hipMemsetAsync(e->k2_cold.p, 0, 64 * sizeof(uint32_t), s));
     }
-    if (!e->h_cold && peak_pick_counts_cold()) {
+    if (!e->h_cold) {
         HIP_TRY(hipHostMalloc((void **)&e->h_cold, sizeof(uint64_t), hipHostMallocMapped));
         *e->h_cold = 0;
         HIP_TRY(hipHostGetDevicePointer((void **)&e->h_cold_dev, e->h_cold, 0));
@@ -637,8 +652,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         {
             ProfScope ps(e, AID_K_STFT, s, true);
             launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false,
-                              e->hotw.p, e->cfg.peak_threshold, (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0,
-                              e->k1_dummy.p, s);
+                              e->hotw.p, e->cfg.peak_threshold, (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0, s);
         }
         if (loc == AID_PCM_HOST) {
             if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
@@ -648,24 +662,18 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         {
             ProfScope ps(e, AID_K_PEAKS, s, true);
             launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
-                             e->mask.p, e->k2_zero.p, e->k2_sink.p, e->k2_cold.p, s);
+                             e->mask.p, e->k2_cold.p, s);
         }
-#ifdef AID_K2_TWICE  // diagnostic: a second K2 over the same rows (cache state after the first)
-        {
-            ProfScope ps(e, AID_K_PEAKS, s, true);
-            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
-                             e->mask.p, e->k2_zero.p, e->k2_sink.p, e->k2_cold.p, s);
-        }
-#endif
-        if (chunks > n_clips) {  // some clip spans several K3 chunks: their bases need the COUNT pass
+        if (multi_chunk) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
-                             false, nullptr, nullptr, 0u, s);
+                             false, nullptr, nullptr, 0u, one_chunk_each, s);
         }
         {
             ProfScope ps(e, AID_K_LANDMARK_WRITE, s, true);
             launch_landmarks(e->mask.p, e->desc.p, n_clips, chunks, e->chunk_counts.p, e->records.p, e->counts.p,
-                             true, e->h_cold_dev ? e->k2_cold.p : nullptr, e->h_cold_dev, (uint32_t)(4 * strips), s);
+                             true, e->h_cold_dev ? e->k2_cold.p : nullptr, e->h_cold_dev, (uint32_t)(4 * strips),
+                             one_chunk_each, s);
         }
     }
     HIP_TRY(hipGetLastError());
@@ -770,7 +778,7 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
         launch_stft_power(d_pcm, d_desc, 1, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
-                          d_out, true, nullptr, e->cfg.peak_threshold, true, nullptr, s);
+                          d_out, true, nullptr, e->cfg.peak_threshold, true, s);
         he = hipGetLastError();
     }
     if (he == hipSuccess) he = hipStreamSynchronize(s);
@@ -782,10 +790,12 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     return AID_OK;
 }
 
-int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips, int64_t n,
-              int32_t noise_a, uint32_t salt, void *stream) {
+int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
+                   int64_t n, int32_t noise_a, uint32_t salt, int32_t fmax_hz, void *stream) {
     if (!e || !dst || !tracks || !starts || n_clips < 0 || n < 0 || noise_a < 0)
         return fail(AID_ERR_INVALID, "aid_synth: bad argument");
+    if (fmax_hz <= 100 || 2 * (int64_t)fmax_hz > e->cfg.sample_rate)
+        return fail(AID_ERR_INVALID, "aid_synth: fmax_hz must be in (100, sample_rate / 2]");
     if (n_clips == 0 || n == 0) return AID_OK;
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
@@ -797,12 +807,17 @@ int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *
     HIP_TRY(hipMemcpyAsync(e->synth_starts.p, starts, n_clips * sizeof(int64_t), hipMemcpyHostToDevice, s));
     {
         ProfScope ps(e, AID_K_SYNTH, s);
-        launch_synth(dst, e->synth_tracks.p, e->synth_starts.p, n_clips, n, e->cfg.sample_rate, noise_a, salt,
+        launch_synth(dst, e->synth_tracks.p, e->synth_starts.p, n_clips, n, e->cfg.sample_rate, noise_a, salt, fmax_hz,
                      e->d_sin, s);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     return AID_OK;
+}
+
+int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips, int64_t n,
+              int32_t noise_a, uint32_t salt, void *stream) {
+    return aid_synth_band(e, dst, tracks, starts, n_clips, n, noise_a, salt, 8000, stream);
 }
 
 int aid_resample_plan(int32_t sr_in, int32_t sr_out, int32_t *up, int32_t *down, int32_t *hl, int32_t *J) {
@@ -1083,11 +1098,20 @@ static int reserve_postings(aid_engine *e, int64_t extra, hipStream_t s) {
     return AID_OK;
 }
 
+// grow the track tables to max_track_plus1 ids; the new tombstone buffer is allocated before anything
+// changes, so a failed growth leaves the engine as it was
 static int ensure_tracks(aid_engine *e, uint32_t max_track_plus1, hipStream_t s) {
     if (max_track_plus1 <= e->n_tracks) return AID_OK;
+    const size_t want = std::max<size_t>(max_track_plus1, 1024);
+    if (want > e->tomb.n) {
+        DevBuf<uint8_t> nb;
+        HIP_TRY(nb.reserve(std::max(want, 2 * e->tomb.n)));
+        if (e->tomb.p) (void)hipDeviceSynchronize();  // in-flight queries may still read the old tombstones
+        std::swap(e->tomb, nb);
+        nb.release();
+    }
+    e->h_tomb.resize(max_track_plus1, 0);
     e->n_tracks = max_track_plus1;
-    e->h_tomb.resize(e->n_tracks, 0);
-    HIP_TRY(e->tomb.reserve(std::max<size_t>(e->n_tracks, 1024)));
     HIP_TRY(hipMemcpyAsync(e->tomb.p, e->h_tomb.data(), e->n_tracks, hipMemcpyHostToDevice, s));
     return AID_OK;
 }
@@ -1364,56 +1388,137 @@ void aid_comm_destroy(aid_comm *c) {
     delete c;
 }
 
+int aid_comm_size(const aid_comm *c, int32_t *world, int32_t *rank) {
+    if (!c || !c->comm) return fail(AID_ERR_INVALID, "aid_comm_size: null comm");
+    int n = 0, r = 0;
+    NCCL_TRY(ncclCommCount(c->comm, &n));
+    NCCL_TRY(ncclCommUserRank(c->comm, &r));
+    if (world) *world = n;
+    if (rank) *rank = r;
+    return AID_OK;
+}
+
+// the exchange in three steps (aid_index_allgather runs them around two RCCL all-gathers; a host-driven
+// exchange, e.g. torch.distributed over gloo, runs them around its own collectives)
+static int shard_info_locked(aid_engine *e, int64_t first, int64_t *count, uint32_t *n_tracks) {
+    if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "index exchange: first out of range");
+    *count = e->n_post - first;
+    *n_tracks = e->n_tracks;
+    return AID_OK;
+}
+
+static int pack_locked(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, hipStream_t s) {
+    const int64_t n = e->n_post - first;
+    if (n > stride) return fail(AID_ERR_INVALID, "aid_index_pack: stride below the shard's count");
+    const uint32_t *src[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
+    for (int q = 0; q < 3 && n > 0; ++q)
+        HIP_TRY(hipMemcpyAsync(planes + q * stride, src[q] + first, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    if (stride > n)  // padding: defined bytes on the wire
+        for (int q = 0; q < 3; ++q)
+            HIP_TRY(hipMemsetAsync(planes + q * stride + n, 0, (stride - n) * sizeof(uint32_t), s));
+    return AID_OK;
+}
+
+// failure-atomic: everything that can fail (growth of the posting planes and track tables) happens before
+// the index changes; the union then replaces [first, n_post) in one stream-ordered pass
+static int splice_locked(aid_engine *e, int64_t first, const uint32_t *recv, int32_t world, int64_t stride,
+                         const int64_t *counts, uint32_t n_tracks, hipStream_t s) {
+    if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "aid_index_splice: first out of range");
+    int64_t tot = 0;
+    for (int r = 0; r < world; ++r) {
+        if (counts[r] < 0 || counts[r] > stride) return fail(AID_ERR_INVALID, "aid_index_splice: bad count");
+        tot += counts[r];
+    }
+    if (first + tot > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index exchange: more than 2^32 postings");
+    // grow keeping every stored posting (n_post, not first: nothing is dropped if this fails)
+    const size_t want = (size_t)std::max<int64_t>(first + tot, e->n_post);
+    if (int rc = grow_copy_u32(e->p_hash, e->n_post, want, s)) return rc;
+    if (int rc = grow_copy_u32(e->p_track, e->n_post, want, s)) return rc;
+    if (int rc = grow_copy_u32(e->p_t, e->n_post, want, s)) return rc;
+    if (int rc = ensure_tracks(e, n_tracks, s)) return rc;
+    uint32_t *dst[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
+    int64_t at = first;
+    for (int r = 0; r < world; ++r) {
+        const int64_t n = counts[r];
+        for (int q = 0; q < 3 && n > 0; ++q)
+            HIP_TRY(hipMemcpyAsync(dst[q] + at, recv + ((size_t)r * 3 + q) * stride, n * sizeof(uint32_t),
+                                   hipMemcpyDeviceToDevice, s));
+        at += n;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    e->n_post = at;
+    e->index_dirty = true;
+    return AID_OK;
+}
+
+int aid_index_shard_info(aid_engine *e, int64_t first, int64_t *count, uint32_t *n_tracks) {
+    if (!e || !count || !n_tracks) return fail(AID_ERR_INVALID, "aid_index_shard_info: null argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return shard_info_locked(e, first, count, n_tracks);
+}
+
+int aid_index_pack(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, void *stream) {
+    if (!e || (!planes && stride > 0) || stride < 0) return fail(AID_ERR_INVALID, "aid_index_pack: bad argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "aid_index_pack: first out of range");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = pick_stream(e, stream);
+    if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    if (int rc = pack_locked(e, first, planes, stride, s)) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    return AID_OK;
+}
+
+int aid_index_splice(aid_engine *e, int64_t first, const uint32_t *recv, int32_t world, int64_t stride,
+                     const int64_t *counts, uint32_t n_tracks, void *stream) {
+    if (!e || world <= 0 || stride < 0 || !counts || (!recv && stride > 0))
+        return fail(AID_ERR_INVALID, "aid_index_splice: bad argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = pick_stream(e, stream);
+    if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    return splice_locked(e, first, recv, world, stride, counts, n_tracks, s);
+}
+
 int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_total) {
     if (!e || !c || !c->comm) return fail(AID_ERR_INVALID, "aid_index_allgather: null argument");
     if (c->device != e->device) return fail(AID_ERR_INVALID, "aid_index_allgather: comm and engine on different devices");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "aid_index_allgather: first out of range");
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->own_stream;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     const int W = c->world;
-    const int64_t n_local = e->n_post - first;
-    // 1. (count, n_tracks) of every rank: sizes the padded exchange and the track tables
+    // 1. (count, n_tracks) of every rank: sizes the padded exchange and the track tables. Every rank takes part
+    //    even when its own arguments are bad (a count of -1 fails all ranks alike instead of leaving them hanging)
+    int64_t n_local = -1;
+    uint32_t nt = 0;
+    const int bad = shard_info_locked(e, first, &n_local, &nt);
     HIP_TRY(e->g_meta.reserve(2 * (size_t)W + 2));
-    const int64_t mine[2] = {n_local, (int64_t)e->n_tracks};
+    const int64_t mine[2] = {bad ? -1 : n_local, (int64_t)nt};
     HIP_TRY(hipMemcpyAsync(e->g_meta.p, mine, sizeof(mine), hipMemcpyHostToDevice, s));
     NCCL_TRY(ncclAllGather(e->g_meta.p, e->g_meta.p + 2, 2, ncclInt64, c->comm, s));
     std::vector<int64_t> meta(2 * (size_t)W);
     HIP_TRY(hipMemcpyAsync(meta.data(), e->g_meta.p + 2, meta.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    int64_t mx = 0, tot = 0, tracks = 0;
+    int64_t mx = 0;
+    uint32_t tracks = 0;
+    std::vector<int64_t> counts(W);
     for (int r = 0; r < W; ++r) {
-        mx = std::max(mx, meta[2 * r]);
-        tot += meta[2 * r];
-        tracks = std::max(tracks, meta[2 * r + 1]);
+        if (meta[2 * r] < 0) return bad ? bad : fail(AID_ERR_INVALID, "aid_index_allgather: another rank's shard is invalid");
+        counts[r] = meta[2 * r];
+        mx = std::max(mx, counts[r]);
+        tracks = std::max(tracks, (uint32_t)meta[2 * r + 1]);
     }
-    if (first + tot > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "aid_index_allgather: more than 2^32 postings");
     if (mx > 0) {
         // 2. own shard as [3][mx] planes (the tail past n_local is padding), one all-gather
         HIP_TRY(e->g_send.reserve(3 * (size_t)mx));
         HIP_TRY(e->g_recv.reserve(3 * (size_t)mx * W));
-        uint32_t *planes[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
-        for (int q = 0; q < 3 && n_local > 0; ++q)
-            HIP_TRY(hipMemcpyAsync(e->g_send.p + q * mx, planes[q] + first, n_local * sizeof(uint32_t),
-                                   hipMemcpyDeviceToDevice, s));
+        if (int rc = pack_locked(e, first, e->g_send.p, mx, s)) return rc;
         NCCL_TRY(ncclAllGather(e->g_send.p, e->g_recv.p, 3 * (size_t)mx, ncclUint32, c->comm, s));
         // 3. the union in rank order replaces this rank's shard
-        e->n_post = first;
-        if (int rc = reserve_postings(e, tot, s)) return rc;
-        if (int rc = ensure_tracks(e, (uint32_t)tracks, s)) return rc;
-        uint32_t *dst[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
-        int64_t at = first;
-        for (int r = 0; r < W; ++r) {
-            const int64_t n = meta[2 * r];
-            for (int q = 0; q < 3 && n > 0; ++q)
-                HIP_TRY(hipMemcpyAsync(dst[q] + at, e->g_recv.p + ((size_t)r * 3 + q) * mx, n * sizeof(uint32_t),
-                                       hipMemcpyDeviceToDevice, s));
-            at += n;
-        }
-        HIP_TRY(hipStreamSynchronize(s));
-        e->n_post = at;
-        e->index_dirty = true;
+        if (int rc = splice_locked(e, first, e->g_recv.p, W, mx, counts.data(), tracks, s)) return rc;
+    } else if (int rc = ensure_tracks(e, tracks, s)) {
+        return rc;
     }
     if (n_total) *n_total = e->n_post;
     return AID_OK;
@@ -1530,14 +1635,12 @@ int aid_index_load(aid_engine *e, const char *path) {
     return AID_OK;
 }
 
+constexpr double kForwardedPerBucket = 2.0;  // forwarded votes (1-bit filter estimate) per global histogram bucket
 // run K5 over nq queries whose records are at device ranges (q_start/q_count device arrays).
 // Exact per-query vote counts (k_query_votes) choose the path and size the vote histogram;
 // queries whose exact LDS table overflowed are re-run with 4x the buckets. (max_recs is unused.)
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
-#ifndef AID_K5_PER_BUCKET
-#define AID_K5_PER_BUCKET 2.0  // forwarded votes (1-bit filter estimate) per global histogram bucket
-#endif
 constexpr int kSpeculateQueries = 16;  // run_queries: LDS match path launched with the vote counts
 
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
@@ -1560,7 +1663,9 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // round trip as the vote counts instead of after them (one host sync less per call). It is exact at
     // any load (an overflowing query reports -1 and falls through to the global path below); only its
     // speed suffers for heavy queries, which a handful of them bounds
-    const bool speculate = e->k5_path == 0 && nq <= kSpeculateQueries;
+    // (gated on the previous batch: a heavy small batch, e.g. stream windows against a large catalog, would
+    // otherwise pay the slow LDS run before falling back every time)
+    const bool speculate = e->k5_path == 0 && nq <= kSpeculateQueries && e->k5_spec_ok;
     std::vector<int32_t> spec_n;
     if (speculate) {
         {
@@ -1587,6 +1692,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     int64_t vmax = 1;
     for (int q = 0; q < nq; ++q) vmax = std::max(vmax, h_votes[q]);
     const double votes = (double)vmax;
+    e->k5_spec_ok = 2.0 * votes <= 65536.0;
     // global histogram, sized for the votes that pass K5a's 2^20-bit seen filter (all but the
     // distinct bits: v - m(1 - e^{-v/m})) at ~2 per bucket: a chance bucket reaching
     // min_match - 1 then has probability ~1e-5. Sizing it for ALL votes (2 buckets each: 2 MB rows on
@@ -1599,7 +1705,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     const double m_seen = (double)(1 << 20), vp = votes / parts;
     const double fwd = parts * (vp - m_seen * (1.0 - std::exp(-vp / m_seen)));
     int bits = 15;
-    while (bits < 24 && (double)(1ull << bits) < fwd / AID_K5_PER_BUCKET) ++bits;
+    while (bits < 24 && (double)(1ull << bits) < fwd / kForwardedPerBucket) ++bits;
     // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is
     // exact for heavier queries too (overflows fall back; tests/test_gpu_match_load.py) but one
     // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~540k
@@ -1723,10 +1829,7 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
     return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, mx, rows, nrows, s);
 }
 
-int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
-    if (!e) return fail(AID_ERR_INVALID, "null engine");
-    if (!e->have_result) return fail(AID_ERR_STATE, "no extraction to query with");
-    std::lock_guard<std::mutex> lk(e->mu);
+static int query_extracted_locked(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
     if (int rc = ensure_index(e)) return rc;
     hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
     const int nq = e->n_clips;
@@ -1735,6 +1838,30 @@ int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
     HIP_TRY(e->q_start.reserve(nq));
     HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
     return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, -1, rows, nrows, s);
+}
+
+int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
+    if (!e) return fail(AID_ERR_INVALID, "null engine");
+    if (!e->have_result) return fail(AID_ERR_STATE, "no extraction to query with");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return query_extracted_locked(e, rows, nrows);
+}
+
+int aid_query_pcm(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
+                  aid_match_row *rows, int32_t *nrows, void *stream) {
+    if (!e || !offsets || n_clips < 0) return fail(AID_ERR_INVALID, "aid_query_pcm: bad argument");
+    if (loc != AID_PCM_HOST && loc != AID_PCM_DEVICE) return fail(AID_ERR_INVALID, "aid_query_pcm: bad pcm_location");
+    if (n_clips > 0 && !pcm && offsets[n_clips] > offsets[0]) return fail(AID_ERR_INVALID, "aid_query_pcm: null pcm");
+    for (int c = 0; c < n_clips; ++c)
+        if (offsets[c + 1] < offsets[c] || offsets[c] < 0)
+            return fail(AID_ERR_INVALID, "aid_query_pcm: offsets must be non-decreasing and >= 0");
+    if (n_clips > 0 && (!rows || !nrows)) return fail(AID_ERR_INVALID, "aid_query_pcm: null output");
+    if (n_clips == 0) return AID_OK;
+    // one critical section: no other thread's extraction can land between this batch's K1-K3 and K5
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = ensure_index(e)) return rc;
+    if (int rc = extract_locked(e, pcm, offsets, n_clips, loc, stream)) return rc;
+    return query_extracted_locked(e, rows, nrows);
 }
 
 }  // extern "C"

@@ -304,29 +304,16 @@ __device__ __forceinline__ void for_each_vote(const QueryParams &qp, int64_t a, 
     });
 }
 
+constexpr int kVoteWindows = 16;  // windows of 64 posting loads a wave keeps in flight
+
 // one wave per query record; its lanes stride over the record's posting list (coalesced)
-#ifndef AID_K5_HIST_THREADS
-#define AID_K5_HIST_THREADS 1024  // 256: 9.4k clips/s on config 4, 1024: 10.3k
-#endif
-#ifndef AID_K5_U
-#define AID_K5_U 16  // 64-posting windows with loads in flight per wave in K5a/K5b (4: 26.9k clips/s, 8: 27.9k, 16: 28.3k)
-#endif
-#ifndef AID_K5_DIAG
-#define AID_K5_DIAG 0  // timing-only K5a variants (wrong results): 1 = no counting, 2 = LDS filter only
-#endif
-#ifndef AID_K5_BLOOM
-#define AID_K5_BLOOM 2  // bits per key in K5a's seen filter (1 or 2, in one 32-bit word)
-#endif
-#ifndef AID_K5_SEEN
-#define AID_K5_SEEN 1  // LDS "seen" pre-filter in front of the global histogram (see k_vote_hist)
-#endif
-// K5a. With AID_K5_SEEN a vote first sets its key's bits in a 2^20-bit LDS "seen" filter (128 KB)
+// K5a. A vote first sets its key's bits in a 2^20-bit LDS "seen" filter (128 KB)
 // and reaches the global histogram only if they were all set already: of a key's c votes at most
 // the first is held back, so a bucket holding a key with c >= min_match votes still counts
 // >= min_match - 1 (K5h tests that). Config 4's windows have ~540k votes each (popular hashes:
 // the vote count is size-biased, ~3x the mean bucket length times the records), and the filter
 // keeps the random global atomics -- the kernel's cost -- to the chance collisions.
-__global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams qp) {
+__global__ __launch_bounds__(1024) void k_vote_hist(QueryParams qp) {
     // qp.parts workgroups per query, each with its own seen filter for one hash partition of the
     // keys: on config 4 (~540k votes) the 2^20-bit filter saturates and lets ~20 % of the votes
     // through to the global histogram; two partitions read every posting twice but forward far
@@ -337,51 +324,28 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t hmask = (1u << qp.hist_bits) - 1;
     uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
-#if AID_K5_SEEN
     __shared__ uint32_t seen[1 << 15];
     for (int i = threadIdx.x; i < (1 << 15); i += blockDim.x) seen[i] = 0u;
     __syncthreads();
-#if AID_K5_DIAG == 1
-    uint32_t acc = 0;  // timing only: enumeration and posting loads, no counting
-    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) { acc ^= mix_td(tr, d); });
-    if (acc == 0x9E3779B1u) H[0] = acc;
-#elif AID_K5_DIAG == 2
-    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
-        const uint32_t x = mix_td(tr, d), b = x >> 12, bit = 1u << (b & 31);
-        atomicOr(&seen[b >> 5], bit);  // timing only: the LDS filter without the global histogram
-    });
-#elif AID_K5_DIAG == 4
-    uint32_t acc = 0;  // timing only: returning LDS filter, no global histogram
-    for_each_vote<AID_K5_U>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
-        const uint32_t x = mix_td(tr, d), b = x >> 12, bit = 1u << (b & 31);
-        acc += (atomicOr(&seen[b >> 5], bit) & bit) ? 1u : 0u;
-    });
-    if (acc == 0x9E3779B1u) H[0] = acc;
-#else
-    // The key's AID_K5_BLOOM bits (a blocked Bloom filter for 2) sit in ONE word, so a single
+    // The key's 2 bits (a blocked Bloom filter) sit in ONE word, so a single
     // atomicOr tests and sets them together: of racing votes of one key exactly one sees a bit
     // clear, so at most the key's first vote is held back, as with one bit. Two bits let fewer
     // chance "seen" collisions through to the global histogram (config 4: 36.9k -> 39.9k clips/s;
     // three bits 38.5k).
-    for_each_vote_batch<AID_K5_U>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
-        uint32_t fw[AID_K5_U];
+    for_each_vote_batch<kVoteWindows>(qp, a, n, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
+        uint32_t fw[kVoteWindows];
 #pragma unroll
-        for (int u = 0; u < AID_K5_U; ++u) {  // all U filter tests first (LDS only)
+        for (int u = 0; u < kVoteWindows; ++u) {  // all filter tests first (LDS only)
             const uint32_t x = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]);
-            uint32_t m = AID_K5_BLOOM > 1 ? (1u << (x & 31)) | (1u << ((x >> 5) & 31)) : 1u << ((x >> 12) & 31);
+            uint32_t m = (1u << (x & 31)) | (1u << ((x >> 5) & 31));
             // a partition's keys (from bits the filter does not use) get the whole filter
             m = ok[u] && ((x >> 10) & (uint32_t)(qp.parts - 1)) == part ? m : 0u;  // parts: 1, 2 or 4
             fw[u] = ((atomicOr(&seen[x >> 17], m) & m) == m && m) ? x & hmask : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int u = 0; u < AID_K5_U; ++u)  // then the global histogram
+        for (int u = 0; u < kVoteWindows; ++u)  // then the global histogram
             if (fw[u] != 0xFFFFFFFFu) atomicAdd(&H[fw[u]], 1u);
     });
-#endif
-#else
-    for_each_vote<4>(qp, a, n, wave, nw, lane,
-                     [&](uint32_t tr, int32_t d, int32_t) { atomicAdd(&H[mix_td(tr, d) & hmask], 1u); });
-#endif
 }
 
 // K5h: one coalesced pass over each query's histogram row: bucket >= min_match -> a bit of the
@@ -390,7 +354,7 @@ __global__ __launch_bounds__(AID_K5_HIST_THREADS) void k_vote_hist(QueryParams q
 // counters from the 2 MB row (a 64-128 B line per 4-byte read: ~46 GB of fetch per 2048 queries).
 __global__ __launch_bounds__(256) void k_hot_scan(QueryParams qp) {
     const int64_t per_q = 1ll << qp.hist_bits;
-    const uint32_t mm = (uint32_t)qp.min_match - (AID_K5_SEEN ? 1u : 0u);  // see k_vote_hist
+    const uint32_t mm = (uint32_t)qp.min_match - 1u;  // the seen filter holds back a key's first vote (k_vote_hist)
     for (int q = blockIdx.y; q < qp.nq; q += gridDim.y) {
         uint32_t *H = qp.hist + ((int64_t)q << qp.hist_bits);
         uint64_t *B = reinterpret_cast<uint64_t *>(qp.hot + ((int64_t)q << (qp.hist_bits - 5)));
@@ -439,7 +403,6 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
         for (int i = tid; i < (1 << (qp.hist_bits - 5)); i += blockDim.x) hotl[i] = hot[i];
     __syncthreads();
     auto insert = [&](uint32_t tr, int32_t d, int32_t tq, uint32_t h) {
-        if (AID_K5_DIAG == 3) { atomicAdd(&vcnt[0], 1u); return; }  // timing only: no exact table
         if (*(volatile int32_t *)&overflow) return;  // the query is re-run on a bigger histogram anyway
         const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
         uint32_t s = (h >> 20) & (kVoteCap - 1);
@@ -457,17 +420,17 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
         }
     };
     auto phase1 = [&](auto word) {
-        for_each_vote_batch<AID_K5_U>(qp, a, z - a, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
-            uint32_t h[AID_K5_U];
-            bool hit[AID_K5_U];
+        for_each_vote_batch<kVoteWindows>(qp, a, z - a, wave, nw, lane, [&](const uint64_t *e, const int32_t *tqs, const bool *ok) {
+            uint32_t h[kVoteWindows];
+            bool hit[kVoteWindows];
 #pragma unroll
-            for (int u = 0; u < AID_K5_U; ++u) {
+            for (int u = 0; u < kVoteWindows; ++u) {
                 h[u] = mix_td((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u]);
                 const uint32_t hb = h[u] & hmask;
                 hit[u] = ok[u] && ((word(hb >> 5) >> (hb & 31)) & 1u);
             }
 #pragma unroll
-            for (int u = 0; u < AID_K5_U; ++u)
+            for (int u = 0; u < kVoteWindows; ++u)
                 if (hit[u]) insert((uint32_t)e[u], (int32_t)(e[u] >> 32) - tqs[u], tqs[u], h[u]);
         });
     };
@@ -746,7 +709,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
                    nrows, tomb_live, hot, parts};
-    hipLaunchKernelGGL(k_vote_hist, dim3(nq * parts), dim3(AID_K5_HIST_THREADS), 0, s, qp);
+    hipLaunchKernelGGL(k_vote_hist, dim3(nq * parts), dim3(1024), 0, s, qp);
     hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
     hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }

@@ -19,45 +19,11 @@
 // clip's record count.
 #include "aidfp_device.h"
 
-#ifndef AID_K3_THREADS
-#define AID_K3_THREADS 512  // 256: 0.055 ms, 512: 0.040, 1024: 0.040 (one workgroup per clip at 256 x 10 s)
-#endif
-
 namespace aid {
 
-constexpr int kK3 = AID_K3_THREADS;  // threads per K3 workgroup
-#ifndef AID_K3_KEEPW
-#define AID_K3_KEEPW 0  // 1: phase 1's mask words stay in registers for phase 2 (<= kK3MaxPer frames per thread)
-#endif
-constexpr int kK3MaxPer = (kHashChunk + kZoneDT + kK3 - 1) / kK3;  // frames per thread in phase 1, at most
+constexpr int kK3 = 512;  // threads per K3 workgroup (256: 0.055 ms, 512: 0.040, 1024: 0.040 at 256 x 10 s)
 
-#ifndef AID_K3_SKIP0
-#define AID_K3_SKIP0 1  // skip the unshuffle of peak-free frames and of empty 256-bin ballot blocks
-                        // (K3 0.0341 -> 0.0268 ms same-box, r02)
-#endif
-
-#ifndef AID_K3_DIAG
-#define AID_K3_DIAG 0  // timing-only ablations (wrong results): 1 = stop after the counts, 2 = after the peak list,
-                       // 3 = after the pair counts
-#endif
-#ifndef AID_K3_SPARSE
-#define AID_K3_SPARSE 1  // expand peaks from the OR of each 256-bin block's ballot words (no unshuffle)
-#endif
-#ifndef AID_K3_DIRECT
-#define AID_K3_DIRECT 1  // one chunk per clip: the workgroup's clip is its chunk index (no binary search)
-#endif
-#ifndef AID_K3_COALESCED
-#define AID_K3_COALESCED 0  // 1: phase 1 reads the mask words coalesced (16 lanes per frame): measured slower (K3 0.0265 -> 0.037 ms; the per-thread runs issue all 32 loads at once)
-#endif
-#ifndef AID_K3_ONEWALK
-#define AID_K3_ONEWALK 1  // the write pass reuses the count walk's accepted targets (first anchor per thread)
-#endif
-
-#ifndef AID_K3_WSCAN
-#define AID_K3_WSCAN 1  // 1: wave scans (shuffles) + one LDS exchange of wave totals: 2 barriers per scan, not 20
-#endif
-
-#if AID_K3_WSCAN
+// exclusive scan of one int64 per thread: wave scans (shuffles) + one LDS exchange of the wave totals
 __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK3]*/, int64_t *total) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     int64_t x = v;  // inclusive scan over the wave
@@ -79,42 +45,6 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK
     __syncthreads();  // every wave has read tmp before the next scan writes it
     return base + x - v;
 }
-#else
-__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t *tmp /*[kK3]*/, int64_t *total) {
-    const int tid = threadIdx.x;
-    tmp[tid] = v;
-    __syncthreads();
-    // Hillis-Steele over kK3 entries (small; runs once per phase)
-    for (int off = 1; off < kK3; off <<= 1) {
-        const int64_t add = tid >= off ? tmp[tid - off] : 0;
-        __syncthreads();
-        tmp[tid] += add;
-        __syncthreads();
-    }
-    const int64_t incl = tmp[tid];
-    if (total) *total = tmp[kK3 - 1];
-    __syncthreads();
-    return incl - v;
-}
-#endif
-
-// bit l of x (l < 16) -> bit 4l
-__device__ __forceinline__ uint64_t spread4(uint64_t x) {
-    x &= 0xFFFFull;
-    x = (x | (x << 24)) & 0x000000FF000000FFull;
-    x = (x | (x << 12)) & 0x000F000F000F000Full;
-    x = (x | (x << 6)) & 0x0303030303030303ull;
-    x = (x | (x << 3)) & 0x1111111111111111ull;
-    return x;
-}
-
-// K2 stores word 4*w + i = ballot over lanes l of bin 256*w + 4*l + i; natural word
-// n (bins 64n .. 64n+63) takes lanes 16*(n&3) .. +15 of the four words of block n>>2.
-__device__ __forceinline__ uint64_t natural_word(const uint64_t (&W)[kMaskWords], int n) {
-    const int blk = 4 * (n >> 2), sh = 16 * (n & 3);
-    return spread4(W[blk + 0] >> sh) | (spread4(W[blk + 1] >> sh) << 1) | (spread4(W[blk + 2] >> sh) << 2) |
-           (spread4(W[blk + 3] >> sh) << 3);
-}
 
 __device__ __forceinline__ uint32_t make_hash(int k1, int k2, int dt) {
     return ((uint32_t)(k1 & 0x3FF) << 22) | ((uint32_t)(k2 & 0x3FF) << 12) | ((uint32_t)dt & 0xFFF);
@@ -125,7 +55,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
                                                   int n_clips, int64_t total_chunks, int64_t *__restrict__ chunk_counts,
                                                   uint64_t *__restrict__ records, int64_t *__restrict__ clip_counts,
                                                   uint32_t *__restrict__ k2_cold, uint64_t *__restrict__ k2_cold_host,
-                                                  uint32_t k2_waves) {
+                                                  uint32_t k2_waves, int one_chunk_each) {
     __shared__ uint32_t plist[kHashChunkPeakCap];
     __shared__ uint32_t foff[kHashChunk + kZoneDT + 2];
     __shared__ int64_t scan_tmp[kK3];
@@ -142,7 +72,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     }
     if (chunk >= total_chunks) return;
     int lo = 0, hi = n_clips - 1;
-    if (AID_K3_DIRECT && total_chunks == n_clips) lo = (int)chunk;  // one chunk per clip: no search
+    if (one_chunk_each) lo = (int)chunk;  // every clip is exactly one chunk (host-checked): no search
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (clips[mid].chunk_base <= chunk) lo = mid; else hi = mid - 1;
@@ -162,38 +92,6 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     const int per = (nf + kK3 - 1) / kK3;
     const int fa = min(tid * per, nf), fz = min(fa + per, nf);
     int64_t mine = 0;
-#if AID_K3_COALESCED
-    // counts read coalesced: 16 consecutive lanes take the 16 mask words of one frame (a wave reads 512
-    // contiguous bytes per load; the per-thread frame runs read 64 scattered 8-B words per load)
-    for (int e = tid; e < nf * kMaskWords; e += kK3) {
-        uint32_t c = (uint32_t)__popcll(Mc[e]);
-        c += __shfl_xor(c, 8, 16);
-        c += __shfl_xor(c, 4, 16);
-        c += __shfl_xor(c, 2, 16);
-        c += __shfl_xor(c, 1, 16);
-        if ((e & (kMaskWords - 1)) == 0) foff[e / kMaskWords] = c;
-    }
-    __syncthreads();
-    for (int f = fa; f < fz; ++f) mine += foff[f];
-#elif AID_K3_KEEPW
-    // the thread's frames' mask words stay in registers for phase 2 (no second round trip to L2/MALL)
-    uint64_t KW[kK3MaxPer][kMaskWords];
-#pragma unroll
-    for (int ff = 0; ff < kK3MaxPer; ++ff) {
-        const int f = fa + ff;
-#pragma unroll
-        for (int w = 0; w < kMaskWords; ++w) KW[ff][w] = f < fz ? Mc[f * kMaskWords + w] : 0ull;
-    }
-#pragma unroll
-    for (int ff = 0; ff < kK3MaxPer; ++ff) {
-        const int f = fa + ff;
-        uint32_t c = 0;
-#pragma unroll
-        for (int w = 0; w < kMaskWords; ++w) c += __popcll(KW[ff][w]);
-        if (f < fz) foff[f] = c;
-        mine += c;
-    }
-#else
     for (int f = fa; f < fz; ++f) {
         uint32_t c = 0;
 #pragma unroll
@@ -201,36 +99,18 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
         foff[f] = c;
         mine += c;
     }
-#endif
     int64_t npk = 0;
     int64_t run = block_excl_scan(mine, scan_tmp, &npk);
-    if (AID_K3_DIAG == 1) return;  // timing only: phase 1 (counts + scan)
-    // 2. expand to the (t,k)-ordered peak list (unshuffling K2's ballot layout)
-#if AID_K3_KEEPW && !AID_K3_COALESCED
-#pragma unroll
-    for (int ff = 0; ff < kK3MaxPer; ++ff) {
-        const int f = fa + ff;
-        if (f >= fz) break;
-#else
+    // 2. expand to the (t,k)-ordered peak list
     for (int f = fa; f < fz; ++f) {
-#endif
         const uint32_t c = foff[f];
         foff[f] = (uint32_t)run;
-#if AID_K3_SKIP0
-        // most frames hold no peak (~0.35 per frame at the bench config), and most 256-bin ballot
-        // blocks of the others are empty: skip the mask reload and the unshuffle for both
+        // most frames hold no peak (~0.35 per frame at the bench config): skip their mask reload
         if (c == 0) continue;
-#endif
         int64_t idx = run;
         uint64_t W[kMaskWords];
 #pragma unroll
-        for (int w = 0; w < kMaskWords; ++w)
-#if AID_K3_KEEPW && !AID_K3_COALESCED
-            W[w] = KW[ff][w];
-#else
-            W[w] = Mc[f * kMaskWords + w];
-#endif
-#if AID_K3_SPARSE
+        for (int w = 0; w < kMaskWords; ++w) W[w] = Mc[f * kMaskWords + w];
         // no unshuffle: a 4-bin group holds at most one peak (FPSPEC 5: no two peaks within +-15 bins), so the
         // OR of a 256-bin block's 4 ballot words has one bit per peak, in ascending bin order; the word
         // holding that bit gives the bin's offset i in the group (bin = 256 b + 4 l + i)
@@ -243,39 +123,18 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
                 plist[idx++] = ((uint32_t)f << 10) | (uint32_t)(256 * b + 4 * l + i);
             }
         }
-#else
-#if AID_K3_SKIP0
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            if ((W[4 * b] | W[4 * b + 1] | W[4 * b + 2] | W[4 * b + 3]) == 0) continue;
-#pragma unroll
-            for (int w = 4 * b; w < 4 * b + 4; ++w) {
-#else
-        {
-            for (int w = 0; w < kMaskWords; ++w) {
-#endif
-                uint64_t m = natural_word(W, w);
-                while (m) {
-                    const int bpos = __ffsll((unsigned long long)m) - 1;
-                    plist[idx++] = ((uint32_t)f << 10) | (uint32_t)(64 * w + bpos);
-                    m &= m - 1;
-                }
-            }
-        }
-#endif
         run += c;
     }
     if (tid == 0) foff[nf] = (uint32_t)npk;
     __syncthreads();
-    if (AID_K3_DIAG == 2) return;  // timing only: phases 1-2 (peak list built)
     const int n_anchor = (int)foff[c1 - c0];
 
     // 3. anchors: contiguous run per thread
     const int pa_per = (n_anchor + kK3 - 1) / kK3;
     const int aa = min(tid * pa_per, n_anchor), az = min(aa + pa_per, n_anchor);
     int64_t my = 0;
-    // the thread's first anchor keeps its accepted targets as a bitmask of walk positions j - i - 1 < 64
-    // (AID_K3_ONEWALK), so the write pass emits them without walking the zone again
+    // the thread's first anchor keeps its accepted targets as a bitmask of walk positions j - i - 1 < 64,
+    // so the write pass emits them without walking the zone again
     uint64_t tmask = 0;
     bool tmask_ok = false;
     for (int i = aa; i < az; ++i) {
@@ -291,13 +150,11 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
             if (dt <= 0) continue;
             const int df = (int)(b & 1023) - ka;
             if (df < -kZoneDF || df > kZoneDF) continue;
-            if (AID_K3_ONEWALK) {
-                if (j - i - 1 < 64) mk |= 1ull << (j - i - 1);
-                else ok = false;
-            }
+            if (j - i - 1 < 64) mk |= 1ull << (j - i - 1);
+            else ok = false;
             ++got;
         }
-        if (AID_K3_ONEWALK && i == aa) {
+        if (i == aa) {
             tmask = mk;
             tmask_ok = ok;
         }
@@ -305,7 +162,6 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
     }
     int64_t chunk_total = 0;
     const int64_t excl = block_excl_scan(my, scan_tmp, &chunk_total);
-    if (AID_K3_DIAG == 3) return;  // timing only: phases 1-3 (pair counts + scan, no records)
     if constexpr (!WRITE) {
         if (tid == 0) chunk_counts[chunk] = chunk_total;
     } else {
@@ -331,7 +187,7 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
             const uint32_t a = plist[i];
             const int ta = (int)(a >> 10), ka = (int)(a & 1023);
             const uint64_t t1 = (uint64_t)(c0 + ta) << 32;
-            if (AID_K3_ONEWALK && i == aa && tmask_ok) {
+            if (i == aa && tmask_ok) {
                 for (uint64_t m = tmask; m; m &= m - 1) {
                     const uint32_t b = plist[i + 1 + (__ffsll((unsigned long long)m) - 1)];
                     out[o++] = t1 | make_hash(ka, (int)(b & 1023), (int)(b >> 10) - ta);
@@ -356,14 +212,16 @@ __global__ __launch_bounds__(kK3) void k_landmarks(const uint64_t *__restrict__ 
 
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
-                      uint64_t *k2_cold_host, uint32_t k2_waves, hipStream_t s) {
+                      uint64_t *k2_cold_host, uint32_t k2_waves, bool one_chunk_each, hipStream_t s) {
     if (total_chunks <= 0) return;
     if (write)
         timed_launch(k_landmarks<true>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
-                           total_chunks, chunk_counts, records, clip_counts, k2_cold, k2_cold_host, k2_waves);
+                           total_chunks, chunk_counts, records, clip_counts, k2_cold, k2_cold_host, k2_waves,
+                     one_chunk_each ? 1 : 0);
     else
         timed_launch(k_landmarks<false>, dim3((unsigned)total_chunks), dim3(kK3), 0, s, mask, clips, n_clips,
-                           total_chunks, chunk_counts, records, clip_counts, (uint32_t *)nullptr, (uint64_t *)nullptr, 0u);
+                           total_chunks, chunk_counts, records, clip_counts, (uint32_t *)nullptr, (uint64_t *)nullptr, 0u,
+                     one_chunk_each ? 1 : 0);
 }
 
 }  // namespace aid

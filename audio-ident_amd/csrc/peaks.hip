@@ -11,8 +11,9 @@
 //
 //   * thread j owns bins 4j..4j+3 (one float4 load per row); the next batch of 4
 //     rows is in flight in registers while the current one is processed;
-//   * rows are staged in LDS 4 at a time (double-buffered, one barrier per 4
-//     rows); each thread reads its +-15-bin neighbours from LDS;
+//   * rows are staged in LDS as int32 keys 4 at a time (one buffer, a barrier before and
+//     after each staging: 21 KB per workgroup, 4+ workgroups per CU), with the maxima of
+//     every 4-bin block; each thread reads its +-15-bin neighbours from LDS;
 //   * the vertical +-7-frame part is register-resident: one sliding maximum M7 of the
 //     row-max over the last 7 rows (from an 8-slot ring of pair maxima, 4 VALU/bin)
 //     gives both `before` of the arriving row (the previous M7, strict) and `after` of
@@ -21,60 +22,16 @@
 //   * a decided row is emitted with 4 wave ballots (one per bin offset i < 4): mask
 //     word 4*w + i of a frame holds, at bit l, the peak flag of bin 256*w + 4*l + i
 //     ("ballot layout"; K3 and aidfp.engine.peaks_from_mask unshuffle it).
+// Only hot 64-bin blocks (K1's per-row hot word) are loaded; a wave whose window blocks are
+// cold in every row of its strip exits at once (it only writes zero mask words).
 // Strips are dealt to workgroups XCD-aware so neighbouring strips (which share
-// halo rows) run on the same XCD's L2.
+// halo rows) run on the same XCD's L2. The variants measured against this layout
+//  live in the git history (commit c236449, the AID_K2_* switches).
 #include "aidfp_device.h"
 
 namespace aid {
 
 constexpr int kRowsPerStep = 4;
-#ifndef AID_K2_REVERSE
-#define AID_K2_REVERSE 1  // 1: last-written strips first (0.2975 -> 0.2930 ms, A/B on one box)
-#endif
-#ifndef AID_K2_BLOCKMAX
-#define AID_K2_BLOCKMAX 1  // horizontal maxima from 4-bin block maxima (see below); 0 = 36 values per thread
-#endif
-#ifndef AID_K2_PF
-#define AID_K2_PF 4  // prefetch distance in rows (4 or 8): rows it+PF .. are in flight in registers
-#endif
-#ifndef AID_K2_COLDSKIP
-#define AID_K2_COLDSKIP 1  // a wave whose +-15-bin neighbourhood is all cold in a row takes a short path
-#endif
-#ifndef AID_K2_ROT
-#define AID_K2_ROT 1  // rotate the wave -> bin-quarter map by blockIdx (SIMD load balance)
-#endif
-#ifndef AID_K2_FULL128
-#define AID_K2_FULL128 1  // whole-block ds_read_b128 for the far blocks j-4 / j+4 instead of ds_read_b96: K2 LDS bank conflicts 8.2 M -> 0 cycles, LDS-array cycles 31.0 M -> 20.2 M; time neutral (0.1910 vs 0.1907 ms)
-#endif
-#ifndef AID_K2_DIAG
-#define AID_K2_DIAG 0  // timing-only: 1 = stage rows but skip the window maxima (peak = p > thr)
-#endif
-#ifndef AID_K2_NBUF
-#define AID_K2_NBUF 1  // row staging buffers: 2 = double-buffered (42 KB LDS: 3 workgroups per CU),
-                       // 1 = single buffer + a second barrier per 4 rows (21 KB: 4 per CU, VGPR-bound):
-                       // K2 0.1908 -> 0.1692 ms, 4.86 -> 5.07 M audio-s/s (same-box A/B, r02)
-#endif
-#ifndef AID_K2_BRANCHFREE
-#define AID_K2_BRANCHFREE 0  // measured slower (K2 0.1709 -> 0.1789 ms: zero-row loads cost more than the branch). 1: row loads of cold blocks read a zero row and the mask store of other lanes/rows
-                             // goes to a dummy sink (per-lane address selects) instead of exec-masked branches
-#endif
-#ifndef AID_K2_MSTORE
-#define AID_K2_MSTORE 1  // mask-word store: 0 = lane-indexed select (hipcc lowered it to a switch of exec-masked
-                         // blocks, ~14 instructions per row), 1 = v_writelane of the SGPR ballots (K2 0.1515 ->
-                         // 0.1427 ms same-box, r02), 2 = lane 0 stores 32 B, 3 = store on every path (2/3: 130
-                         // VGPRs, occupancy 3)
-#endif
-#ifndef AID_K2_WCOLD
-#define AID_K2_WCOLD 1  // 1: a wave whose window blocks are cold in every row of the strip skips the row loop
-                        // (K2 0.1418 -> 0.1302-0.1350 ms same-box, r02; needs AID_K2_MIN_WAVES 4: 130 VGPRs
-                        // otherwise, occupancy 3)
-#endif
-#ifndef AID_K2_WCOLD_EXIT
-#define AID_K2_WCOLD_EXIT 1  // 1: a strip-cold wave exits after zeroing its LDS bins and mask words
-#endif
-#ifndef AID_K2_MIN_WAVES
-#define AID_K2_MIN_WAVES 4  // 4 caps VGPRs at 128 (occupancy 4; no spills since r02: 122 VGPRs with AID_K2_WCOLD)
-#endif
 
 // Peak decisions compare powers as int32 keys: a power is >= +0 (never -0: FPSPEC 4's
 // fma(Xr, Xr, Xi*Xi), stored unscaled as 4P by K1), and non-negative binary32 values order exactly like their bit
@@ -82,9 +39,6 @@ constexpr int kRowsPerStep = 4;
 // neighbour never raises a maximum) and `!(p > thr)` (a NaN is never a peak); +inf keeps its
 // bits. Integer max needs no NaN canonicalisation: hipcc put a `v_max_f32 x, x, x` in front of
 // ~19 of the ~65 fmaxf operands of every row.
-#ifndef AID_K2_FMAXKEY
-#define AID_K2_FMAXKEY 1  // K2 0.1709 -> 0.1623 ms same-box (r02). 1: the key is the bits of v_max_f32(0, x) (maxNum: a NaN gives 0, +-0 gives +0)
-#endif
 template <int LANE>
 __device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t s_val) {  // v[LANE] = s_val (uniform)
     asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s_val), "i"(LANE));
@@ -92,33 +46,25 @@ __device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t s_val) {  //
 }
 
 __device__ __forceinline__ int pkey(float x) {
-#if AID_K2_FMAXKEY
     // one VALU instead of v_cmp + v_cndmask (+ the VCC hazard's s_nop). Same keys: the plane holds K1's
     // fma results (quiet NaNs, no sNaN, no negative non-NaN values), and maxNum(qNaN, 0) = 0
     float r;
     asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
     return __float_as_int(r);
-#else
-    const uint32_t b = __float_as_uint(x);
-    return b <= 0x7F800000u ? (int)b : 0;
-#endif
 }
 
-__global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
+// occupancy 4 forced by the launch bounds (<= 128 VGPRs, no spills)
+__global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
                                                   const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask,
-                                                  const float4 *__restrict__ zero_row, uint64_t *__restrict__ sink,
                                                   uint32_t *__restrict__ cold_cnt) {
-    __shared__ __attribute__((aligned(16))) int rows[AID_K2_NBUF][kRowsPerStep][kBins + 32];
-#if AID_K2_BLOCKMAX
-    __shared__ __attribute__((aligned(16))) int bms[AID_K2_NBUF][kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
-#endif
+    __shared__ __attribute__((aligned(16))) int rows[kRowsPerStep][kBins + 32];  // keys, 16 pads each side
+    __shared__ __attribute__((aligned(16))) int bms[kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
     // wave = the 256-bin quarter of the row this wave owns, rotated by the workgroup index: the
     // waves of a workgroup go to the CU's 4 SIMDs in order, so without rotation every workgroup's
     // low-frequency (hot) quarter lands on SIMD 0 and its cold top quarter on SIMD 3
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(AID_K2_ROT ? (((int)(threadIdx.x >> 6) + (int)blockIdx.x) & 3)
-                                                               : (int)(threadIdx.x >> 6));
+    const int wave = __builtin_amdgcn_readfirstlane(((int)(threadIdx.x >> 6) + (int)blockIdx.x) & 3);
     const int tid = wave * 64 + lane;  // owner of bins 4 tid .. 4 tid + 3
     constexpr int kInf = 0x7F800000;  // key of +inf
 
@@ -128,14 +74,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
         const int64_t nb = gridDim.x, b = blockIdx.x;
         const int64_t per = nb / 8, rem = nb % 8, x = b % 8, y = b / 8;
         strip = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
-#if AID_K2_REVERSE
         strip = nb - 1 - strip;  // last-written power rows (still in the MALL after K1) first
-#endif
     }
     if (strip >= total_strips) return;
-#if AID_K2_DIAG == 3
-    if (strip >= 0) return;  // launch + strip deal only
-#endif
     int lo = 0, hi = n_clips - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -148,30 +89,19 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     const int t1 = min(t0 + strip_len, F);
     const float *P = power + fb * kBins;
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
-#if AID_K2_BRANCHFREE || AID_K2_MSTORE == 3
-    uint64_t *sinkw = sink + (int64_t)(blockIdx.x & (kK2SinkBlocks - 1)) * 256 + threadIdx.x;  // other stores
-    (void)zero_row;
-#else
-    (void)sink;
-    (void)zero_row;
-#endif
     // K1's plane holds Q = 4P (stft.hip, real split): compare against 4 thr (exact: thr <= 2^100)
     const int kthr = __float_as_int(4.0f * thr);            // thr > 0 (engine config check)
 
     if (tid < 16) {
 #pragma unroll
-        for (int b = 0; b < AID_K2_NBUF; ++b)
-#pragma unroll
-            for (int r = 0; r < kRowsPerStep; ++r) {
-                rows[b][r][tid] = 0;
-                rows[b][r][kBins + 16 + tid] = 0;
-#if AID_K2_BLOCKMAX
-                if (tid < 4) {
-                    bms[b][r][tid] = 0;
-                    bms[b][r][260 + tid] = 0;
-                }
-#endif
+        for (int r = 0; r < kRowsPerStep; ++r) {
+            rows[r][tid] = 0;
+            rows[r][kBins + 16 + tid] = 0;
+            if (tid < 4) {
+                bms[r][tid] = 0;
+                bms[r][260 + tid] = 0;
             }
+        }
     }
 
     // vertical +-7 as one sliding max: M7(s) = max row-max (fm) over rows s-6..s, built from
@@ -197,18 +127,9 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
     // Words are fetched one step ahead of the row loads they gate (scalar loads)
     const uint32_t *HW = hot + fb;
     const int myb = tid >> 4;
-#if AID_K2_BRANCHFREE
-    // clamped scalar load + select: no branch around the s_load for rows outside the clip
-    auto hotword = [&](int r) -> uint32_t {
-        const uint32_t w = HW[min(max(r, 0), F - 1)];
-        return (r >= 0 && r < F) ? w : 0u;
-    };
-#else
     auto hotword = [&](int r) -> uint32_t { return (r >= 0 && r < F) ? HW[r] : 0u; };
-#endif
     // blocks 4w-1 .. 4w+4 hold the wave's bins and their +-15 neighbours
     const uint32_t wmask = (0x3Fu << (4 * wave)) >> 1;
-#if AID_K2_WCOLD
     {
         // strip-cold wave: if those blocks are cold in every row the strip reads, every key this wave
         // stages or compares is 0, so it has no candidate and its mask words are 0 (exact, as the
@@ -218,51 +139,32 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
         for (int r = rbeg + lane; r < rbeg + iters; r += 64) acc |= (r >= 0 && r < F) ? HW[r] : 0u;
         if (__ballot((acc & wmask) != 0u) == 0) {
 #pragma unroll
-            for (int b = 0; b < AID_K2_NBUF; ++b)
-#pragma unroll
-                for (int j = 0; j < kRowsPerStep; ++j) {
-                    reinterpret_cast<int4 *>(&rows[b][j][16])[tid] = make_int4(0, 0, 0, 0);
-#if AID_K2_BLOCKMAX
-                    bms[b][j][4 + tid] = 0;
-#endif
-                }
+            for (int j = 0; j < kRowsPerStep; ++j) {
+                reinterpret_cast<int4 *>(&rows[j][16])[tid] = make_int4(0, 0, 0, 0);
+                bms[j][4 + tid] = 0;
+            }
             uint64_t *Mz = mask + fb * kMaskWords + 4 * wave + (lane & 3);
             for (int r = t0 + (lane >> 2); r < t1; r += 16) Mz[(int64_t)r * kMaskWords] = 0;
-#if AID_K2_WCOLD_EXIT
             // the wave terminates: s_barrier waits only for a workgroup's surviving waves, and its
-            // registers go to waves of workgroups still waiting for a slot (host: AIDFP_K2_SLOTS_X); its
+            // registers go to waves of workgroups still waiting for a slot (host: extract_locked); its
             // zeroed LDS bins are written before it ends. The cold waves are counted (64 counters, read
             // and reset by K3) so the host can size the next call's strips (extract_locked)
             if (lane == 0 && cold_cnt) atomicAdd(&cold_cnt[blockIdx.x & 63], 1u);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             return;
-#else
-            for (int it = 0; it < iters; it += kRowsPerStep) {
-                if (AID_K2_NBUF == 1 && it > 0) __syncthreads();
-                __syncthreads();
-            }
-            return;
-#endif
         }
     }
-#endif
-    float4 pf[AID_K2_PF];  // rows of the next batch(es), in flight
+    float4 pf[kRowsPerStep];  // rows of the next step, in flight
 #pragma unroll
-    for (int j = 0; j < AID_K2_PF; ++j) {
+    for (int j = 0; j < kRowsPerStep; ++j) {
         const int r = rbeg + j;
-#if AID_K2_BRANCHFREE
-        pf[j] = ((j < iters && ((hotword(r) >> myb) & 1u)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)
-                                                            : zero_row)[tid];
-#else
         pf[j] = (j < iters && ((hotword(r) >> myb) & 1u)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
                                                           : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
     }
     uint32_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
 #pragma unroll
-    for (int j = 0; j < kRowsPerStep; ++j) hw[j] = hotword(rbeg + AID_K2_PF + j);
+    for (int j = 0; j < kRowsPerStep; ++j) hw[j] = hotword(rbeg + kRowsPerStep + j);
     // hot words of the rows in flight (hsave) and of the rows being processed (hcur)
-    static_assert(!AID_K2_COLDSKIP || AID_K2_PF == kRowsPerStep, "cold skip tracks rows one step ahead");
     uint32_t hsave[kRowsPerStep], hcur[kRowsPerStep];
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) hsave[j] = hcur[j] = hotword(rbeg + j);
@@ -272,65 +174,31 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
         for (int s = 0; s < 8; ++s) {
             const int it = base + s;
             if (it >= iters) break;  // workgroup-uniform
-            const int buf = AID_K2_NBUF == 1 ? 0 : (it / kRowsPerStep) & 1;
-            if (AID_K2_DIAG != 2 && s % kRowsPerStep == 0) {
-                if (AID_K2_NBUF == 1 && it > 0) __syncthreads();  // every wave is done with the previous 4 rows
+            if (s % kRowsPerStep == 0) {
+                if (it > 0) __syncthreads();  // every wave is done with the previous 4 rows
                 // stage rows it .. it+3 as keys, then fetch rows it+PF .. (register staging beats
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll
                 for (int j = 0; j < kRowsPerStep; ++j) {
-                    const int slot = (s + j) % AID_K2_PF;  // compile-time: the loop is unrolled by 8
+                    const int slot = (s + j) % kRowsPerStep;  // compile-time: the loop is unrolled by 8
                     const float4 v = pf[slot];
                     const int4 kv = make_int4(pkey(v.x), pkey(v.y), pkey(v.z), pkey(v.w));
-                    reinterpret_cast<int4 *>(&rows[buf][j][16])[tid] = kv;
-#if AID_K2_BLOCKMAX
-                    bms[buf][j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
-#endif
-                    const int rn = rbeg + it + j + AID_K2_PF;
+                    reinterpret_cast<int4 *>(&rows[j][16])[tid] = kv;
+                    bms[j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
+                    const int rn = rbeg + it + j + kRowsPerStep;
                     hcur[j] = hsave[j];
                     hsave[j] = hw[j];
-#if AID_K2_BRANCHFREE
-                    // a cold block (or a row past the strip) reads the zero row: one load per lane, no branch
-                    pf[slot] = ((it + j + AID_K2_PF < iters && ((hw[j] >> myb) & 1u))
-                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)
-                                    : zero_row)[tid];
-#else
-                    pf[slot] = (it + j + AID_K2_PF < iters && ((hw[j] >> myb) & 1u))
+                    pf[slot] = (it + j + kRowsPerStep < iters && ((hw[j] >> myb) & 1u))
                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
                     hw[j] = hotword(rn + kRowsPerStep);
                 }
                 __syncthreads();
             }
             const int r = rbeg + it;
-#if AID_K2_DIAG == 2
-            {
-                // loads only: no LDS staging, no keys
-                const float4 v = pf[s % AID_K2_PF];
-                const int x = __float_as_int(v.x) ^ __float_as_int(v.y) ^ __float_as_int(v.z) ^ __float_as_int(v.w);
-                const uint64_t b0 = __ballot(x == 0x12345);
-                if (r >= t0 && r < t1 && lane < 4) M[(int64_t)r * kMaskWords] = b0;
-                const int rn = rbeg + it + AID_K2_PF;
-                pf[s % AID_K2_PF] = (it + AID_K2_PF < iters && rn >= 0 && rn < F)
-                                        ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-                continue;
-            }
-#endif
-#if AID_K2_DIAG == 1
-            {
-                const int4 me = reinterpret_cast<const int4 *>(rows[buf][s % kRowsPerStep])[tid + 4];
-                const uint64_t b0 = __ballot(me.x > kthr), b1 = __ballot(me.y > kthr), b2 = __ballot(me.z > kthr),
-                               b3 = __ballot(me.w > kthr);
-                if (r >= t0 && r < t1 && lane < 4)
-                    M[(int64_t)r * kMaskWords] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-                continue;
-            }
-#endif
             bool pk[4];
             uint64_t bal[4];  // ballots of pk, taken where pk is computed (SGPR results, no 0/1 VGPRs)
-            if (AID_K2_COLDSKIP && !(hcur[s % kRowsPerStep] & wmask)) {
+            if (!(hcur[s % kRowsPerStep] & wmask)) {
                 // every key the wave's windows see is 0: fm = 0, no candidate (p = 0 is never > the
                 // threshold); only the vertical ring advances and row r-7 is decided
 #pragma unroll
@@ -345,21 +213,15 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                     pend[s][i] = -1;
                 }
             } else {
-#if !AID_K2_BLOCKMAX
-            const int *rb = rows[buf][s % kRowsPerStep];
-#endif
-#if AID_K2_BLOCKMAX
             // thread j owns block j = bins 4j..4j+3. Its +-15 windows span blocks j-4..j+4: the
             // far blocks j-4 / j+4 contribute a suffix / prefix of their bins, blocks j+-1..3 whole
             // (their maxima, staged with the row), the own block a prefix / suffix -- 18 max ops
             // per thread and row instead of 46, and 2 x 16 B + 6 x 4 B of LDS reads instead of 9 x 16 B
-            const int4 *rb4 = reinterpret_cast<const int4 *>(rows[buf][s % kRowsPerStep]);
-            const int *bm = bms[buf][s % kRowsPerStep];
+            const int4 *rb4 = reinterpret_cast<const int4 *>(rows[s % kRowsPerStep]);
+            const int *bm = bms[s % kRowsPerStep];
             const int4 lf = rb4[tid], me = rb4[tid + 4], rt = rb4[tid + 8];  // blocks j-4, j, j+4
-#if AID_K2_FULL128
             // keep lf.x / rt.w live so hipcc issues ds_read_b128, not ds_read_b96 (lf uses bins 1..3, rt 0..2)
             asm volatile("" ::"v"(lf.x), "v"(rt.w));
-#endif
             const int M3L = max(max(bm[tid + 1], bm[tid + 2]), bm[tid + 3]);  // blocks j-3..j-1
             const int M3R = max(max(bm[tid + 5], bm[tid + 6]), bm[tid + 7]);  // blocks j+1..j+3
             const int lsuf2 = max(lf.z, lf.w), lsuf1 = max(lf.y, lsuf2);      // block j-4: bins 1..3, 2..3
@@ -375,40 +237,13 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             R[1] = max(max(msuf2, M3R), rt.x);
             R[2] = max(max(me.w, M3R), rpre1);
             R[3] = max(M3R, rpre2);
-            int q[36];
-            q[16] = me.x; q[17] = me.y; q[18] = me.z; q[19] = me.w;
-#else
-            int q[36];  // bins 4j-16 .. 4j+19 (zero outside the frame)
-#pragma unroll
-            for (int v = 0; v < 9; ++v) {
-                const int4 w = reinterpret_cast<const int4 *>(rb)[tid + v];
-                q[4 * v + 0] = w.x; q[4 * v + 1] = w.y; q[4 * v + 2] = w.z; q[4 * v + 3] = w.w;
-            }
-            // keep the two unused edge values live: otherwise hipcc re-pairs the used ones into
-            // ds_read2_b32 at a 16-byte lane stride (8-way bank conflict) instead of 9 ds_read_b128
-            asm volatile("" ::"v"(q[0]), "v"(q[35]));
-            // own bin i is q[16+i]; left window q[1+i..15+i], right window q[17+i..31+i]
-            int midL = q[4], midR = q[20];
-#pragma unroll
-            for (int u = 5; u <= 15; ++u) midL = max(midL, q[u]);
-#pragma unroll
-            for (int u = 21; u <= 31; ++u) midR = max(midR, q[u]);
-            int L[4], R[4];
-            L[0] = max(max(q[1], q[2]), max(q[3], midL));
-            L[1] = max(max(q[2], q[3]), max(midL, q[16]));
-            L[2] = max(max(q[3], midL), max(q[16], q[17]));
-            L[3] = max(max(midL, q[16]), max(q[17], q[18]));
-            R[0] = max(max(q[17], q[18]), max(q[19], midR));
-            R[1] = max(max(q[18], q[19]), max(midR, q[32]));
-            R[2] = max(max(q[19], midR), max(q[32], q[33]));
-            R[3] = max(max(midR, q[32]), max(q[33], q[34]));
-#endif
+            const int mev[4] = {me.x, me.y, me.z, me.w};
 
             // candidates only inside the strip's output rows (uniform): other rows get +inf
             const int thr_row = (r >= t0 && r < t1) ? kthr : kInf;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int p = q[16 + i];
+                const int p = mev[i];
                 const int fm = max(max(L[i], p), R[i]);
                 const int m2 = max(fm, fprev[i]);
                 fprev[i] = fm;
@@ -426,24 +261,7 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
             }
             const uint64_t b0 = bal[0], b1 = bal[1], b2 = bal[2], b3 = bal[3];
             const int rd = r - kPeakDT;
-#if AID_K2_BRANCHFREE
-            {
-                const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-                uint64_t *dstw = (rd >= t0 && rd < t1 && lane < 4) ? M + (int64_t)rd * kMaskWords : sinkw;
-                *dstw = wv;
-            }
-#elif AID_K2_MSTORE == 3
-            {
-                // one mask store per row on every path (a row outside the strip goes to the sink): the
-                // store count between a row fetch and its use is then the same on every path, so the
-                // wait before staging is vmcnt(4) instead of a vmcnt(0) that also waited for the stores
-                const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-                uint64_t *dstw = (rd >= t0 && rd < t1) ? M + (int64_t)rd * kMaskWords : sinkw;
-                if (lane < 4) *dstw = wv;
-            }
-#else
             if (rd >= t0 && rd < t1) {
-#if AID_K2_MSTORE == 1
                 // lane i < 4 stores ballot word i: 8 v_writelane of the SGPR ballots
                 uint32_t lo = 0, hi = 0;
                 lo = write_lane<0>(lo, (uint32_t)b0);
@@ -455,33 +273,17 @@ __global__ __launch_bounds__(256, AID_K2_MIN_WAVES) void k_peak_pick(const float
                 lo = write_lane<3>(lo, (uint32_t)b3);
                 hi = write_lane<3>(hi, (uint32_t)(b3 >> 32));
                 if (lane < 4) M[(int64_t)rd * kMaskWords] = ((uint64_t)hi << 32) | lo;
-#elif AID_K2_MSTORE == 2
-                // the wave's 4 words are contiguous (word 4 wave + i): lane 0 stores all 32 bytes
-                if (lane == 0) {
-                    uint4 *d = reinterpret_cast<uint4 *>(M + (int64_t)rd * kMaskWords);
-                    d[0] = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
-                    d[1] = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
-                }
-#else
-                if (lane < 4) {
-                    const uint64_t wv = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
-                    M[(int64_t)rd * kMaskWords] = wv;
-                }
-#endif
             }
-#endif
         }
     }
 }
 
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
-                      float thr, const uint32_t *hot, uint64_t *mask, const float *zero_row, uint64_t *sink,
-                      uint32_t *cold_cnt, hipStream_t s) {
+                      float thr, const uint32_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {
     if (total_strips <= 0) return;
     timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
-                       strip_len, thr, hot, mask, reinterpret_cast<const float4 *>(zero_row), sink, cold_cnt);
+                 strip_len, thr, hot, mask, cold_cnt);
 }
-bool peak_pick_counts_cold() { return AID_K2_WCOLD && AID_K2_WCOLD_EXIT; }
 
 // resident K2 workgroups per CU (registers / LDS), for sizing strips to one round
 int peak_pick_blocks_per_cu() {

@@ -78,13 +78,7 @@ __global__ __launch_bounds__(kResThreads) void k_resample(const float *__restric
 // 8-tap chunk (L1-resident table) and runs kResR dot products with them. Per output that is
 // J input reads from LDS (+ J / kResR tap loads) instead of 2J LDS reads with per-lane phase
 // rows (which also bank-conflicted). Same fma chain per output (taps j = 0..J-1 in order).
-#ifndef AID_RS_PHASE
-#define AID_RS_PHASE 1
-#endif
-#ifndef AID_RS_R
-#define AID_RS_R 16
-#endif
-constexpr int kResR = AID_RS_R;  // outputs per thread (one phase)
+constexpr int kResR = 16;  // outputs per thread (one phase)
 
 template <bool STEREO>
 __global__ __launch_bounds__(256) void k_resample_phase(const float *__restrict__ src, int64_t in_base, int64_t n,
@@ -142,7 +136,7 @@ __global__ __launch_bounds__(256) void k_resample_phase(const float *__restrict_
 // phase-major blocks hold up * kResR outputs: used while that window stays small (common rate
 // pairs: up = 147, 160, 441); very large up (near-coprime rates) keep the 1024-output blocks
 static bool use_phase(int up, int down, int J) {
-    return AID_RS_PHASE && up > 1 && up <= 1024 && ((int64_t)up * kResR - 1) * down / up + J + 2 <= 12288;
+    return up > 1 && up <= 1024 && ((int64_t)up * kResR - 1) * down / up + J + 2 <= 12288;
 }
 
 static int64_t window_floats(int up, int down, int J) {

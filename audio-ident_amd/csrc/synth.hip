@@ -60,13 +60,13 @@ __global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, const ui
 }
 
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
-                  int noise_a, uint32_t salt, const int16_t *sin_tab, hipStream_t s) {
+                  int noise_a, uint32_t salt, int fmax_hz, const int16_t *sin_tab, hipStream_t s) {
     if (n <= 0 || n_clips <= 0) return;
     SynthParams sp;
     sp.n = n;
     sp.note_len = sr / 4;
     sp.inc_min = (uint32_t)floor(100.0 / sr * 4294967296.0);
-    sp.inc_rng = (uint32_t)floor(7900.0 / sr * 4294967296.0);
+    sp.inc_rng = (uint32_t)floor((double)(fmax_hz - 100) / sr * 4294967296.0);  // partials in [100, fmax_hz) Hz
     sp.noise_a = noise_a;
     sp.salt = salt;
     sp.seed_mul = (uint32_t)((42ull * 0x9E3779B9ull) & 0xFFFFFFFFull);

@@ -4,17 +4,25 @@
 Workload (BASELINE.json configs[1]): a batch of 256 x 10 s
 44.1 kHz mono synthetic clips, resident in HBM (generated on the device by
 aid_synth). One step = one pass of K1 stft_power -> K2 peak_pick -> K3
-landmark_hash (count + write) over the whole batch through the C ABI.
+landmark_hash over the whole batch through the C ABI.
 
 N GPUs: one process per GPU (torch.distributed, RCCL backend), each rank
 fingerprints its own 256-clip batch (extraction shards by clip, no data-path
 collective: weak scaling). value = audio-seconds of all ranks / max-rank time.
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts the N
+ranks itself (a child `torch.distributed.run`, before anything touches the GPU)
+and exits with its status; under a launcher WORLD_SIZE must equal --gpus.
 
-Roofline: the dominant kernel's algorithmic HBM bytes per launch (DESIGN.md
-"Roofline") / its mean launch time from HIP events recorded on the launch
-stream during the timed region, against 8.0 TB/s. cpu_baseline: the C oracle
-(oracle/fp_oracle.c, bit-exact restatement) on rank 0 at N=1 over a bounded
-sample of the same clips.
+Extra keys of the line (none of them is `value`):
+  * roofline -- the dominant kernel's algorithmic HBM bytes per launch / its mean launch
+    time from HIP events on the launch stream in the timed region, against 8.0 TB/s; plus
+    which unit binds: traffic_frac (PMC bytes) and valu_issue_frac (SQ_INSTS_VALU) per
+    extraction kernel, from the newest committed profiles/;
+  * fullband -- the same batch with partials up to 20 kHz (no cold upper blocks);
+  * catalog -- BASELINE config 3: 100k x 30 s tracks sharded over the ranks, extract +
+    the RCCL all-gather of the postings (aid_index_allgather) + the index build;
+  * cpu_baseline -- the bit-exact C oracle on the host cores, and the NumPy/SciPy path, on
+    rank 0 at N=1 over bounded samples of the same clips.
 """
 
 from __future__ import annotations
@@ -22,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -36,10 +46,36 @@ SR = 44100
 CLIPS = 256
 CLIP_S = 10
 HBM_PEAK_GBS = 8000.0
+SIMDS = 1024          # 256 CUs x 4 SIMDs (MI355X_MICROARCH)
+CLOCK_HZ = 2.4e9      # max engine clock
+VALU_CYCLES = 2       # a wave64 VALU instruction issues over 2 cycles on a SIMD-32
+KERNEL_SQ = {"stft_power": "k_stft_power", "peak_pick": "k_peak_pick", "landmark_write": "k_landmarks"}
+KERNEL_PMC = {"stft_power": "stft_power", "peak_pick": "peak_pick", "landmark_write": "landmarks"}
+
+
+def launch_plan(gpus: int, env) -> str:
+    """'run' in this process, 'spawn' N ranks, or 'error' (a launcher started another world size)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "run"
+    return "run" if int(ws) == gpus else "error"
+
+
+def spawn_ranks(gpus: int) -> int:
+    """`torch.distributed.run` with one rank per GPU as a CHILD process (never an exec: this process has not
+    touched the GPU and does not), forwarding our arguments; returns its exit status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
 
 
 def algorithmic_bytes(frames: int, samples: int) -> dict:
-    """Per-launch algorithmic HBM bytes of each extraction kernel (DESIGN.md)."""
+    """Per-launch algorithmic HBM bytes of each extraction kernel (SURVEY.md 8(d), DESIGN.md 4)."""
     return {
         # K1 reads every PCM sample once, writes 1024 fp32 bins per frame
         "stft_power": 4 * samples + 4 * 1024 * frames,
@@ -48,17 +84,59 @@ def algorithmic_bytes(frames: int, samples: int) -> dict:
     }
 
 
-def load_pmc(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if present."""
+def load_pmc() -> tuple[dict, str | None]:
+    """HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) from the newest committed PMC
+    summary: {kernel: bytes}."""
     for f in sorted((ROOT / "profiles").glob("pmc_*.json"), reverse=True):
         try:
-            d = json.loads(f.read_text())
-            k = d.get("kernels", {}).get(kernel)
-            if k and k.get("hbm_bytes_per_launch"):
-                return float(k["hbm_bytes_per_launch"]), f.name
+            d = json.loads(f.read_text()).get("kernels", {})
+            out = {k: float(d[v]["hbm_bytes_per_launch"]) for k, v in KERNEL_PMC.items()
+                   if v in d and d[v].get("hbm_bytes_per_launch")}
+            if out:
+                return out, f.name
         except Exception:
             continue
-    return None, None
+    return {}, None
+
+
+def load_sq() -> tuple[dict, str | None]:
+    """SQ_INSTS_VALU (and the rest) per launch from the newest committed SQ summary (sq_*.txt lines
+    `<dir> <kernel> <counter> n= <n> mean=<v>`): {kernel: {counter: mean}}."""
+    for f in sorted((ROOT / "profiles").glob("sq_*.txt"), reverse=True):
+        out: dict = {}
+        try:
+            for ln in f.read_text().splitlines():
+                parts = ln.split()
+                if len(parts) >= 5 and parts[-1].startswith("mean="):
+                    out.setdefault(parts[1], {})[parts[2]] = float(parts[-1][5:])
+        except Exception:
+            continue
+        if any("SQ_INSTS_VALU" in v for v in out.values()):
+            return out, f.name
+    return {}, None
+
+
+def cpu_info() -> dict:
+    """Host CPU model and the cores this process may use: the affinity set, capped by a cgroup CPU quota
+    (a GPU box shows the whole machine's CPUs to nproc but grants a share)."""
+    model = "unknown"
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = visible if quota is None else max(1, min(visible, int(quota)))
+    return {"model": model, "cpus_visible": visible, "cgroup_quota_cpus": quota, "cores": usable}
 
 
 def parity(eng, host_pcm: np.ndarray, ref=None) -> dict:
@@ -77,13 +155,15 @@ def parity(eng, host_pcm: np.ndarray, ref=None) -> dict:
 
 
 def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
-    """The C oracle on the host cores over the bench batch: passes of all 256 clips on `threads` threads until
-    `min_s` seconds have elapsed (>= 1 pass; ~10 s of CPU work with the single-thread leg), then 64 clips on
-    one thread. Returns the oracle's records of the batch (for the parity check) and the baseline dict."""
+    """The C oracle on the host cores over the bench batch: passes of all 256 clips on every usable core until
+    `min_s` seconds have elapsed (>= 1 pass), then 64 clips on one thread; then the NumPy/SciPy path
+    (oracle.fingerprint_numpy) over 16 clips on one process and on a process pool. Returns the oracle's
+    records of the batch (for the parity check) and the baseline dict."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O  # checker / CPU baseline only
 
-    threads = min(16, os.cpu_count() or 1)
+    ci = cpu_info()
+    threads = ci["cores"]
     sample = host_pcm[: min(len(host_pcm), 256)]
     O.fingerprint_batch(sample[:2], 512, threads=1)  # warm (tables)
     passes = 0
@@ -100,15 +180,199 @@ def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
     dt_1 = time.perf_counter() - t
     audio_mt = passes * sample.shape[0] * sample.shape[1] / SR
     audio_1 = one.shape[0] * one.shape[1] / SR
+    np_leg = numpy_baseline(sample[:16], threads)
     return ref, {
         "value": round(audio_mt / dt_mt, 1),
         "unit": "audio-s/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": ci["model"],
+        "cpus_visible": ci["cpus_visible"],
+        "cgroup_quota_cpus": ci["cgroup_quota_cpus"],
         "sample": f"{passes} pass(es) over the {sample.shape[0]} x {CLIP_S} s clips of the same batch through "
                   f"oracle/fp_oracle.c (bit-exact C restatement, -O2) on {threads} host threads ({dt_mt:.1f} s); "
                   f"single-thread {audio_1 / dt_1:.1f} audio-s/s over {one.shape[0]} clips ({dt_1:.1f} s)",
+        "single_thread": round(audio_1 / dt_1, 1),
+        "numpy_scipy": np_leg,
     }
+
+
+def _np_worker(args):
+    x, hop = args
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+
+    return O.fingerprint_numpy(x, hop)
+
+
+def numpy_baseline(clips: np.ndarray, procs: int) -> dict:
+    """oracle.fingerprint_numpy (float64 rfft + scipy.ndimage.maximum_filter + vectorised pairing): one
+    process (pocketfft is single-threaded), then a process pool of `procs` workers."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+
+    O.fingerprint_numpy(clips[0], 512)  # warm (scipy import)
+    t = time.perf_counter()
+    for x in clips[:4]:
+        O.fingerprint_numpy(x, 512)
+    dt1 = time.perf_counter() - t
+    audio1 = 4 * clips.shape[1] / SR
+    work = [(clips[i % len(clips)], 512) for i in range(max(len(clips), 2 * procs))]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        pool.map(_np_worker, work[:procs])  # start-up
+        t = time.perf_counter()
+        pool.map(_np_worker, work)
+        dtp = time.perf_counter() - t
+    return {"value_1proc": round(audio1 / dt1, 1), "value_pool": round(len(work) * clips.shape[1] / SR / dtp, 1),
+            "procs": procs, "unit": "audio-s/s",
+            "sample": f"4 clips on one process ({dt1:.1f} s), {len(work)} clips on {procs} processes ({dtp:.1f} s)",
+            "note": "float64 NumPy/SciPy restatement of FPSPEC 4-6 (oracle.fingerprint_numpy); its records equal "
+                    "the oracle's on the synthetic clips (tests/test_oracle.py), but it is not the bit-exact checker"}
+
+
+def roofline_units(kern: dict, pmc: dict, sq: dict) -> dict:
+    """Per extraction kernel: which unit binds, from the committed counters and this run's durations."""
+    out = {}
+    for k, v in kern.items():
+        ms = v.get("ms_per_launch")
+        if not ms:
+            continue
+        d = {"ms_per_launch": round(ms, 5)}
+        if k in pmc:
+            d["traffic_bytes"] = pmc[k]
+            d["traffic_gbs"] = round(pmc[k] / (ms * 1e-3) / 1e9, 1)
+            d["traffic_frac"] = round(pmc[k] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        c = sq.get(KERNEL_SQ.get(k, ""), {})
+        if "SQ_INSTS_VALU" in c:
+            d["valu_insts"] = c["SQ_INSTS_VALU"]
+            d["valu_issue_frac"] = round(c["SQ_INSTS_VALU"] * VALU_CYCLES / (SIMDS * CLOCK_HZ * ms * 1e-3), 4)
+        if "SQ_INSTS_LDS" in c:
+            d["lds_insts"] = c["SQ_INSTS_LDS"]
+        out[k] = d
+    return out
+
+
+def run_steps(eng, pcm_ptr, offs, stream, steps, torch):
+    for _ in range(steps):
+        eng.extract_device(pcm_ptr, offs, stream)
+    torch.cuda.synchronize()
+
+
+def settle(eng, pcm_ptr, offs, stream, seconds, torch) -> int:
+    """Keep stepping (untimed) until the GPU has been busy for `seconds`: an idle MI355X needs ~25 ms of
+    load to reach its steady clocks (probes/ramp_probe.py)."""
+    n = 0
+    t = time.perf_counter()
+    while time.perf_counter() - t < seconds:
+        run_steps(eng, pcm_ptr, offs, stream, 10, torch)
+        n += 10
+    return n
+
+
+def breakdown(eng, pcm_ptr, offs, stream, steps, torch) -> dict:
+    """Untimed pass with events on every extraction kernel: {kernel: (ms, launches)}."""
+    eng.profile_select(None)
+    eng.profile_enable(True)
+    eng.profile_read(reset=True)
+    run_steps(eng, pcm_ptr, offs, stream, steps, torch)
+    prof = eng.profile_read(reset=True)
+    eng.profile_enable(False)
+    return {k: {"ms_per_launch": ms / cnt, "launches": cnt} for k, (ms, cnt) in prof.items() if cnt}
+
+
+def fullband_leg(eng, pcm, offs, stream, args, rank, torch, dist) -> dict:
+    """The same batch shape with partials in [100, 20000) Hz: every 64-bin block up to ~20 kHz is hot, so
+    K1 stores and K2 loads the whole band (the headline data stops at 8 kHz, ~60 % cold blocks)."""
+    tracks = np.arange(CLIPS, dtype=np.uint32) + np.uint32(rank * CLIPS + 500000)
+    n = SR * CLIP_S
+    eng.synth(pcm.data_ptr(), tracks, np.zeros(CLIPS, np.int64), n, fmax_hz=20000)
+    run_steps(eng, pcm.data_ptr(), offs, stream, max(1, args.warmup), torch)
+    settle(eng, pcm.data_ptr(), offs, stream, args.settle, torch)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_steps(eng, pcm.data_ptr(), offs, stream, args.steps, torch)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    el = _max_over_ranks(el, dist, torch)
+    world = dist.get_world_size() if dist else 1
+    kern = breakdown(eng, pcm.data_ptr(), offs, stream, max(1, min(args.steps, 20)), torch)
+    out = {"value": round(world * CLIPS * CLIP_S * args.steps / el, 1), "unit": "audio-s/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4), "hashes_per_step_per_gpu": int(eng.counts().sum()),
+           "kernels": {k: round(v["ms_per_launch"], 5) for k, v in kern.items()},
+           "data": "aid_synth_band fmax 20 kHz (same seed rules, track ids offset by 500000)"}
+    if rank == 0:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle as O  # checker only
+
+        host = pcm.view(CLIPS, n)[:4].cpu().numpy()
+        ref = O.fingerprint_batch(host, 512, threads=min(8, os.cpu_count() or 1))
+        out["parity"] = {"clips": 4, "bit_exact": all(np.array_equal(eng.hashes(c), ref[c]) for c in range(4))}
+    return out
+
+
+def _max_over_ranks(x: float, dist, torch) -> float:
+    if not dist:
+        return x
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def catalog_leg(args, rank, world, dist, torch) -> dict:
+    """BASELINE config 3: args.catalog_tracks x args.catalog_seconds synthetic tracks, shard(rank) generated and
+    fingerprinted on each GPU, the postings replicated by ONE exchange (native aid_index_allgather over RCCL;
+    under the gloo rehearsal, pack/splice around gloo), then the full CSR built on every GPU. value = the job's
+    audio-seconds / the slowest rank's ingest time (extract + exchange + build; on-device generation excluded,
+    reported apart), as bench_catalog.py."""
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.engine import Engine
+
+    exchange = "native" if (not dist or dist.get_backend() == "nccl") else "torch"
+    eng = Engine(SR, device=torch.cuda.current_device())
+    try:
+        tracks = np.arange(args.catalog_tracks, dtype=np.uint32)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = ingest_synthetic(eng, tracks, args.catalog_seconds, batch=1024, exchange=exchange)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        ph = [wall - st.t_synth, st.t_extract - st.t_synth, st.t_exchange, st.t_build, st.t_comm_init, st.t_synth]
+        if dist:
+            on_dev = dist.get_backend() == "nccl"
+            t = torch.tensor(ph, dtype=torch.float64, device="cuda" if on_dev else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ph = t.tolist()
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, int(st.postings_local))
+        else:
+            per_rank = [int(st.postings_local)]
+        ingest, te, tx, tb, ti, tsyn = ph
+        stats = eng.index_stats()
+        audio = args.catalog_tracks * args.catalog_seconds
+        gathered = 12 * sum(per_rank)  # bytes of (hash, track, t) every rank receives
+        return {"value": round(audio / ingest, 1), "unit": "audio-s/s", "tracks": args.catalog_tracks,
+                "track_seconds": args.catalog_seconds, "ingest_s": round(ingest, 4),
+                "phase_s_max_over_ranks": {"extract": round(te, 4), "allgather": round(tx, 4), "build": round(tb, 4),
+                                           "comm_init": round(ti, 4), "synth_generation": round(tsyn, 4)},
+                "exchange": st.exchange, "rccl_nranks": st.rccl_nranks or None,
+                "postings_per_rank": per_rank, "postings_union": int(st.postings_total),
+                "postings_held": int(stats["postings"]), "postings_live": int(stats["live"]),
+                "allgather_bytes_per_rank": gathered,
+                "allgather_gbs_per_rank": round(gathered / tx / 1e9, 1) if world > 1 and tx > 0 else None,
+                "union_equals_sum_of_shards": int(st.postings_total) == sum(per_rank)}
+    finally:
+        eng.close()
 
 
 def main() -> int:
@@ -119,13 +383,41 @@ def main() -> int:
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--settle", type=float, default=0.1,
                     help="seconds of untimed steps after the warmup steps (GPU clock ramp); 0 = none")
+    ap.add_argument("--no-fullband", action="store_true", help="skip the full-band workload key")
+    ap.add_argument("--no-catalog", action="store_true", help="skip the config-3 catalog leg")
+    ap.add_argument("--catalog-tracks", type=int, default=100000)
+    ap.add_argument("--catalog-seconds", type=float, default=30.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks, print one line per rank and exit without touching the GPU (tests)")
     args = ap.parse_args()
+
+    plan = launch_plan(args.gpus, os.environ)
+    if plan == "error":
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr)
+        return 2
+    if plan == "spawn":
+        return spawn_ranks(args.gpus)
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        import torch.distributed as dist
+
+        line = {"dry_run": True, "rank": rank, "world": world, "local_rank": local}
+        if world > 1:
+            dist.init_process_group("gloo")
+            line["world"] = dist.get_world_size()
+            for r in range(line["world"]):  # one rank at a time: whole lines on the shared stdout
+                if r == rank:
+                    print(json.dumps(line), flush=True)
+                dist.barrier()
+            dist.destroy_process_group()
+        else:
+            print(json.dumps(line), flush=True)
+        return 0
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -139,6 +431,8 @@ def main() -> int:
         else:
             torch.cuda.set_device(local % torch.cuda.device_count())
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     else:
         torch.cuda.set_device(0)
 
@@ -153,25 +447,13 @@ def main() -> int:
     stream = torch.cuda.current_stream().cuda_stream
     frames = CLIPS * eng.num_frames(n)
 
-    for _ in range(max(0, args.warmup)):
-        eng.extract_device(pcm.data_ptr(), offs, stream)
-    torch.cuda.synchronize()
-    # settle: keep stepping (untimed) until the GPU has been busy for SETTLE_S. An idle MI355X
-    # needs ~25 ms of load to reach its steady clocks: the first 20 steps after start-up (or after
-    # 0.5 s idle) ran K1 at 0.345 ms against 0.303 ms steady (probes/ramp_probe.py)
-    settle_steps = 0
-    t_settle = time.perf_counter()
-    while time.perf_counter() - t_settle < args.settle:
-        for _ in range(10):
-            eng.extract_device(pcm.data_ptr(), offs, stream)
-        settle_steps += 10
-        torch.cuda.synchronize()
+    run_steps(eng, pcm.data_ptr(), offs, stream, max(0, args.warmup), torch)
+    settle_steps = settle(eng, pcm.data_ptr(), offs, stream, args.settle, torch)
     hashes_per_step = int(eng.counts().sum())
 
     # events inside the timed region on K1 (stft_power, the dominant kernel) only: every timed launch
     # carries two dispatch-attached events, ~6 us of end-of-kernel work per launch on MI355X
-    # (probes/prof_overhead.py: 4.72 M audio-s/s with K1-K3 timed, 4.82 M with K1 only, 4.86 M with
-    # none). The per-kernel breakdown comes from an untimed pass after the timed region.
+    # (probes/prof_overhead.py). The per-kernel breakdown comes from an untimed pass after the timed region.
     eng.profile_select([0])
     eng.profile_enable(True)
     eng.profile_read(reset=True)
@@ -186,35 +468,23 @@ def main() -> int:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof = eng.profile_read(reset=True)
-    # untimed breakdown pass: every extraction kernel gets events
-    eng.profile_select(None)
-    for _ in range(max(1, min(args.steps, 20))):
-        eng.extract_device(pcm.data_ptr(), offs, stream)
-    torch.cuda.synchronize()
-    prof_all = eng.profile_read(reset=True)
     eng.profile_enable(False)
-
-    if dist:
-        on_dev = dist.get_backend() == "nccl"
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_dev else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    kern = {k: {**v, "pass": "untimed breakdown"}
+            for k, v in breakdown(eng, pcm.data_ptr(), offs, stream, max(1, min(args.steps, 20)), torch).items()}
+    for k, (ms, cnt) in prof.items():  # the timed region's own events win where they exist
+        if cnt:
+            kern[k] = {"ms_per_launch": ms / cnt, "launches": cnt, "pass": "timed region"}
+    elapsed = _max_over_ranks(elapsed, dist, torch)
 
     audio_s = world * CLIPS * CLIP_S * args.steps
     value = audio_s / elapsed
-
-    live = {k: {"ms_per_launch": (ms / cnt if cnt else None), "launches": cnt} for k, (ms, cnt) in prof.items() if cnt}
-    kern = {k: {"ms_per_launch": (ms / cnt if cnt else None), "launches": cnt, "pass": "untimed breakdown"}
-            for k, (ms, cnt) in prof_all.items() if cnt}
-    for k, v in live.items():  # the timed region's own events win where they exist
-        kern[k] = {**v, "pass": "timed region"}
     alg = algorithmic_bytes(frames, CLIPS * n)
-    # dominant kernel from the breakdown pass; its duration from the timed region when it was timed there
-    dom = max(("stft_power", "peak_pick"),
-              key=lambda k: prof_all[k][0] / prof_all[k][1] if k in prof_all and prof_all[k][1] else 0.0)
+    dom = max(("stft_power", "peak_pick"), key=lambda k: kern[k]["ms_per_launch"] if k in kern else 0.0)
     dom_ms = kern[dom]["ms_per_launch"]
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9
-    pmc, pmc_src = load_pmc(dom)
+    pmc, pmc_src = load_pmc()
+    sq, sq_src = load_sq()
+    units = roofline_units(kern, pmc, sq)
     roofline = {
         "kernel": dom,
         "bound": "hbm",
@@ -222,20 +492,29 @@ def main() -> int:
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": pmc,
+        "traffic": pmc.get(dom),
         "algorithmic_bytes_per_launch": alg[dom],
-        "traffic_source": pmc_src,
+        "duration_ms": round(dom_ms, 5),
         "duration_source": kern[dom]["pass"],
-        "extraction_kernels_ms_per_step": round(sum(v["ms_per_launch"] for v in kern.values() if v["ms_per_launch"]), 4),
+        "traffic_frac": units.get(dom, {}).get("traffic_frac"),
+        "valu_issue_frac": units.get(dom, {}).get("valu_issue_frac"),
+        "per_kernel": units,
+        "traffic_source": pmc_src,
+        "sq_source": sq_src,
+        "extraction_kernels_ms_per_step": round(sum(v["ms_per_launch"] for v in kern.values()), 4),
         # the whole step against the same staged-dataflow accounting (K1 + K2 bytes of SURVEY 8(d); K3's
         # mask reads and record writes are < 1 % and left out): how far the pipeline is from streaming
         "step_staged_bytes": alg["stft_power"] + alg["peak_pick"],
         "step_achieved": round((alg["stft_power"] + alg["peak_pick"]) / (elapsed / args.steps) / 1e9, 1),
-        "note": "achieved = SURVEY 8(d) staged-dataflow bytes (PCM + the full power plane); K1 stores only hot "
-                "64-bin blocks and K2 reads only those, so the PMC traffic can be below the algorithmic bytes",
+        "note": "frac = SURVEY 8(d) staged-dataflow bytes (PCM + the full power plane) / the kernel's time. K1 "
+                "stores only hot 64-bin blocks and K2 reads only those, so the bytes actually moved (traffic, PMC "
+                "2 x FETCH_SIZE + WRITE_SIZE) are below that on band-limited audio: traffic_frac says how busy HBM "
+                "is, valu_issue_frac (SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x 2.4 GHz x duration)) how busy the "
+                "vector issue is -- the larger of the two is the binding unit",
     }
 
     cpu = par = None
+    host = None
     if rank == 0:
         host = pcm.view(CLIPS, n).cpu().numpy()
         ref = None
@@ -243,6 +522,20 @@ def main() -> int:
             ref, cpu = cpu_baseline(host)
         # untimed: the batch's hashes (from the last step) against the oracle's
         par = parity(eng, host, ref)
+
+    fullband = None
+    if not args.no_fullband:
+        fullband = fullband_leg(eng, pcm, offs, stream, args, rank, torch, dist)
+    del pcm
+    eng.close()
+    torch.cuda.empty_cache()
+
+    catalog = None
+    if not args.no_catalog:
+        try:
+            catalog = catalog_leg(args, rank, world, dist, torch)
+        except Exception as exc:  # the headline stands on its own
+            catalog = {"error": f"{type(exc).__name__}: {exc}"}
 
     if rank == 0:
         line = {
@@ -265,21 +558,26 @@ def main() -> int:
                 "clip_seconds": CLIP_S,
                 "sample_rate": SR,
                 "n_fft": 2048,
-                "hop": eng.hop,
-                "parallelism": f"replicas x{world} (clip-sharded, no collective)",
+                "hop": 512,
+                "parallelism": f"clip-sharded x{world} (no data-path collective)",
+                "process_group": dist.get_backend() if dist else None,
             },
             "realtime_factor_per_gpu": round(value / world, 1),
             "hashes_per_step_per_gpu": hashes_per_step,
             "kernels": kern,
             "roofline": roofline,
+            "fullband": fullband,
+            "catalog": catalog,
             "cpu_baseline": cpu,
             "parity": par,
         }
         print(json.dumps(line), flush=True)
-    eng.close()
     if dist:
         dist.destroy_process_group()
-    return 0 if par is None or par["bit_exact"] else 1
+    ok = par is None or par["bit_exact"]
+    if fullband and "parity" in fullband:
+        ok = ok and fullband["parity"]["bit_exact"]
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

@@ -14,9 +14,13 @@
  * hipStream_t passed as void* (NULL = the engine's own stream, a blocking stream:
  * it is ordered after work the caller queued on the legacy default stream, so
  * buffers produced there are complete before the engine reads them). An engine is
- * bound to one GPU; calls on one engine must be serialised by the caller except
- * where noted (the Python adapter holds a lock, like the reference's single
- * LMDB writer, fingerprint.py:7-8).
+ * bound to one GPU and takes an internal lock per call, so calls from several
+ * threads never corrupt it; but a SEQUENCE of calls that shares state (aid_extract
+ * then aid_result_* / aid_index_add_extracted / aid_query_extracted) must not be
+ * interleaved with another thread's extraction. The single-call readers aid_query_pcm
+ * and aid_exact_lane have no such window. The Python adapter takes a reader/writer
+ * lock: index writers exclusive (the reference's single LMDB writer,
+ * fingerprint.py:7-8), concurrent readers shared.
  */
 #ifndef AIDFP_H
 #define AIDFP_H
@@ -84,6 +88,15 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out);
 void aid_engine_destroy(aid_engine *e);
 int aid_engine_config(const aid_engine *e, aid_config *out);
 
+/* Test hook: force one of the engine's own code paths, which it otherwise chooses itself per call
+   (the parity tests run every path against the oracle). Never needed in production. */
+#define AID_FORCE_K5_PATH 1        /* 0 auto, 1 LDS vote table first, 2 global histogram only */
+#define AID_FORCE_K5_PARTS 2       /* 0 by vote count, else 1, 2 or 4 key partitions per query (K5a) */
+#define AID_FORCE_K5_BATCH 3       /* 0 default (2048), else global-path queries per launch */
+#define AID_FORCE_K2_STRIPS_X100 4 /* 0 adaptive, else 100 x K2 strips per resident workgroup slot */
+#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix-sort build, 2 atomic counting-sort build */
+int aid_engine_force(aid_engine *e, int32_t what, int32_t value);
+
 /* Frames and worst-case record count of a clip of n samples (FPSPEC 1, 5). */
 int64_t aid_num_frames(const aid_engine *e, int64_t n_samples);
 int64_t aid_hash_capacity(const aid_engine *e, int64_t n_samples);
@@ -124,6 +137,10 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
    [n_clips][n]: tracks/starts are HOST arrays; noise_a = query-noise half-width (0 = none). */
 int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips, int64_t n,
               int32_t noise_a, uint32_t salt, void *stream);
+/* Same with the partials' band [100, fmax_hz) Hz instead of [100, 8000) (fmax_hz <= sample_rate / 2): the
+   bench's full-band workload, whose spectrum has no cold upper blocks. aid_synth = fmax_hz 8000. */
+int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
+                   int64_t n, int32_t noise_a, uint32_t salt, int32_t fmax_hz, void *stream);
 
 /* ---- index + match (FPSPEC 7) ----
  * Replaces `olaf_c store` + LMDB (fingerprint.py:117-125), `olaf_c del` (:239-246) and
@@ -212,6 +229,17 @@ void aid_comm_destroy(aid_comm *c);
  * the union in rank order; postings before `first` stay. The index is left dirty (finalize
  * next). *n_total = postings now held. Every rank must call it with the same comm. */
 int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_total);
+/* The communicator's RCCL view: ranks (ncclCommCount) and this rank (ncclCommUserRank). */
+int aid_comm_size(const aid_comm *c, int32_t *world, int32_t *rank);
+/* aid_index_allgather in three steps, for an exchange the host runs itself (e.g. torch.distributed,
+ * gloo on host copies). Every rank: aid_index_shard_info -> all-gather (count, n_tracks) -> stride = max
+ * count -> aid_index_pack its shard into DEVICE planes [3][stride] (hash, track, t; zero padding) ->
+ * all-gather the planes into DEVICE recv [world][3][stride] -> aid_index_splice with the host counts
+ * [world] and max n_tracks. Splice is failure-atomic: on error the index is unchanged. */
+int aid_index_shard_info(aid_engine *e, int64_t first, int64_t *count, uint32_t *n_tracks);
+int aid_index_pack(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, void *stream);
+int aid_index_splice(aid_engine *e, int64_t first, const uint32_t *recv, int32_t world, int64_t stride,
+                     const int64_t *counts, uint32_t n_tracks, void *stream);
 
 /* Flat versioned file (magic AIDFPIX1 + header + posting columns + tombstones): replaces the OLAF_DB dir. */
 int aid_index_save(aid_engine *e, const char *path);
@@ -222,6 +250,13 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
               int32_t *nrows);
 /* Query with every clip of the last aid_extract (records stay on the device). */
 int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows);
+/* Extraction + query of a batch of clips as ONE call (offsets/pcm as aid_extract; rows [n_clips][max_results],
+   nrows [n_clips], host): safe to call from several threads at once -- the engine serialises the calls and no
+   other call's extraction can interleave. The reader entry point of the Python service, which coalesces
+   concurrent olaf_query requests into one call (replaces one `olaf_c query` process per request,
+   fingerprint.py:185-193). Synchronous. */
+int aid_query_pcm(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t pcm_location,
+                  aid_match_row *rows, int32_t *nrows, void *stream);
 
 /* Batched exact lane: replaces app/search/exact.py run_exact_lane's
    sub-window fan-out, the olaf_query calls and the consensus (exact.py:70-124, :132-353) for a

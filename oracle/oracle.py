@@ -209,6 +209,66 @@ def logmag_f64(x: np.ndarray, hop: int) -> np.ndarray:
     return 10.0 * np.log10(stft_power_f64(x, hop) + 1e-10)
 
 
+# ---------------------------------------------------------------- NumPy/SciPy CPU path (timing baseline)
+
+def fingerprint_numpy(x: np.ndarray, hop: int, thr: float = DEFAULT_THR) -> np.ndarray:
+    """FPSPEC 4-6 written the way a NumPy/SciPy user would (BASELINE north_star: "the reference
+    NumPy/SciPy CPU path"; the reference itself has none): framed float64 rfft
+    (pocketfft), scipy.ndimage.maximum_filter over the 15 x 31 neighbourhood with the earliest-wins
+    tie rule applied to the few tied maxima, vectorised anchor/target pairing. It is the bench's
+    cpu_baseline "numpy_scipy" leg only: float64 arithmetic, so its records are not bit-exact with
+    the binary32 spec (fp_oracle.c is the checker); `tests/test_oracle.py` bounds the difference."""
+    from scipy.ndimage import maximum_filter
+
+    P = stft_power_f64(x, hop)
+    F = P.shape[0]
+    if F == 0:
+        return np.zeros(0, dtype=np.uint64)
+    mx = maximum_filter(P, size=(15, 31), mode="constant", cval=-1.0)
+    cand = (P == mx) & (P > thr)
+    cand[:, 0] = False
+    # ties: of two candidates in each other's neighbourhood (equal maxima) the later in (t, k) order loses
+    from scipy.ndimage import uniform_filter
+
+    crowd = uniform_filter(cand.astype(np.float64), size=(15, 31), mode="constant") * (15 * 31) > 1.5
+    t, k = np.nonzero(cand)  # (t, k) order
+    tied = np.nonzero(crowd[t, k])[0]
+    if len(tied) > 1:
+        keep = np.ones(len(t), dtype=bool)
+        for a_, i in enumerate(tied):
+            if not keep[i]:
+                continue
+            o = tied[a_ + 1:]
+            near = (np.abs(t[o] - t[i]) <= 7) & (np.abs(k[o] - k[i]) <= 15)
+            keep[o[near]] = False
+        t, k = t[keep], k[keep]
+    n = len(t)
+    if n < 2:
+        return np.zeros(0, dtype=np.uint64)
+    # pairing: anchor i with the peaks i+1 .. i+D in order (the target zone spans < 64 frames)
+    D = int(min(n - 1, 64 * 64))
+    out_h, out_t, out_i, out_j = [], [], [], []
+    taken = np.zeros(n, dtype=np.int64)
+    for d in range(1, D + 1):
+        i = np.arange(n - d)
+        j = i + d
+        dt = t[j] - t[i]
+        if dt.min() > 63:
+            break
+        ok = (dt > 0) & (dt <= 63) & (np.abs(k[j] - k[i]) <= 127) & (taken[i] < 10)
+        taken[i[ok]] += 1
+        ii, jj = i[ok], j[ok]
+        out_h.append((k[ii].astype(np.uint64) << 22) | (k[jj].astype(np.uint64) << 12) | (t[jj] - t[ii]).astype(np.uint64))
+        out_t.append(t[ii].astype(np.uint64))
+        out_i.append(ii)
+        out_j.append(jj)
+    if not out_h:
+        return np.zeros(0, dtype=np.uint64)
+    h, ta, ai, aj = (np.concatenate(v) for v in (out_h, out_t, out_i, out_j))
+    order = np.lexsort((aj, ai))  # anchor, then target order
+    return h[order] | (ta[order] << np.uint64(32))
+
+
 if os.environ.get("AIDFP_ORACLE_AUTOBUILD", "1") == "1" and not LIB_PATH.exists():
     try:
         build()

@@ -1,7 +1,11 @@
-"""The N>1 catalog exchange (aidfp.catalog.allgather_postings) under the gloo
-backend on CPU, world_size 2 and 3: variable counts, an empty rank, rank-order
-concatenation, u32 bit patterns carried through int32 tensors. The GPU path runs
-the same function over RCCL (bench_catalog.py)."""
+"""The N>1 catalog exchange protocol (aidfp.catalog.exchange_postings) under the gloo backend on
+CPU, world_size 2 and 3: counts first, one max-padded all-gather, splice in rank order, an empty
+rank, u32 bit patterns carried through int32 tensors, postings before `first` kept.
+
+The engine steps it drives (aid_index_shard_info / aid_index_pack / aid_index_splice) are stood in
+for by `HostEngine`, a numpy model of their contract (include/aidfp.h); the real ones run the same
+protocol on the GPU in tests/test_gpu_comm.py (two ranks on one GPU over gloo) and inside
+aid_index_allgather over RCCL (bench.py --gpus N, bench_catalog.py)."""
 
 import os
 import socket
@@ -12,7 +16,49 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from aidfp.catalog import allgather_postings, shard
+from aidfp.catalog import exchange_postings, shard
+
+
+class HostEngine:
+    """numpy model of the exchange's three C ABI steps on a host posting store [n, 3]."""
+
+    def __init__(self, post: np.ndarray, n_tracks: int):
+        self.post = post.astype(np.uint32)
+        self.n_tracks = n_tracks
+        self._bufs = {}
+
+    def alloc_planes(self, k):
+        t = torch.zeros(max(k, 1), dtype=torch.int32)
+        self._bufs[t.data_ptr()] = t
+        return t[:k] if k else t[:0]
+
+    def _view(self, ptr):
+        for base, t in self._bufs.items():
+            if base <= ptr < base + 4 * t.numel():
+                return t.numpy().view(np.uint32)[(ptr - base) // 4:]
+        raise AssertionError("unknown buffer")
+
+    def index_shard_info(self, first):
+        return len(self.post) - first, self.n_tracks
+
+    def index_pack(self, first, ptr, stride):
+        v = self._view(ptr)
+        n = len(self.post) - first
+        assert n <= stride
+        for q in range(3):
+            v[q * stride: q * stride + n] = self.post[first:, q]
+            v[q * stride + n: (q + 1) * stride] = 0
+
+    def index_splice(self, first, ptr, counts, stride, n_tracks):
+        parts = [self.post[:first]]
+        if stride:
+            v = self._view(ptr)
+            for r, n in enumerate(counts):
+                blk = v[r * 3 * stride: (r + 1) * 3 * stride].reshape(3, stride)
+                parts.append(blk[:, :n].T)
+        self.post = np.concatenate(parts, axis=0).astype(np.uint32)
+        self.n_tracks = max(self.n_tracks, n_tracks)
+        return len(self.post)
 
 
 def _free_port():
@@ -29,37 +75,45 @@ def _blocks(world):
     out = []
     for r, n in enumerate(sizes):
         b = rng.integers(0, 2**32, size=(n, 3), dtype=np.uint64).astype(np.uint32)
-        b[:, 1] = r  # track column encodes the rank
+        b[:, 1] = 100 * r + np.arange(n)  # track column: rank-owned ids
         out.append(b)
     return out
+
+
+KEEP = np.array([[1, 2, 3], [4, 5, 6]], np.uint32)  # postings before `first`, identical on every rank
 
 
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        mine = torch.from_numpy(_blocks(world)[rank].astype(np.int32))
-        got = allgather_postings(mine)
-        q.put((rank, got.numpy().astype(np.uint32)))
+        mine = _blocks(world)[rank]
+        eng = HostEngine(np.concatenate([KEEP, mine]), n_tracks=100 * rank + len(mine))
+        total = exchange_postings(eng, first=len(KEEP))
+        q.put((rank, total, eng.post, eng.n_tracks))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_allgather_postings_gloo(world):
+def test_exchange_postings_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = {r: (t, post, nt) for r, t, post, nt in (q.get(timeout=120) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    expect = np.concatenate(_blocks(world), axis=0)
+    expect = np.concatenate([KEEP] + _blocks(world), axis=0)
+    nt_max = max(100 * r + len(b) for r, b in enumerate(_blocks(world)))
     for r in range(world):
-        assert np.array_equal(res[r], expect)
+        total, post, nt = res[r]
+        assert total == len(expect)
+        assert np.array_equal(post, expect)
+        assert nt == nt_max
 
 
 def test_shard_balanced_and_complete():

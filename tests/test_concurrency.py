@@ -1,0 +1,71 @@
+"""aidfp.concurrency: the reader/writer lock and the query coalescer (CPU, no engine)."""
+
+import threading
+import time
+
+import pytest
+
+from aidfp.concurrency import QueryCoalescer, RWLock
+
+
+def test_rwlock_readers_share_writer_excludes():
+    lk = RWLock()
+    lk.acquire_read()
+    lk.acquire_read()  # two readers at once
+    got = []
+    w = threading.Thread(target=lambda: (lk.acquire_write(), got.append("w"), lk.release_write()))
+    w.start()
+    time.sleep(0.05)
+    assert got == []  # the writer waits for both readers
+    r3 = []
+    t3 = threading.Thread(target=lambda: (lk.acquire_read(), r3.append(1), lk.release_read()))
+    t3.start()
+    time.sleep(0.05)
+    assert r3 == []  # writer preference: a new reader queues behind the waiting writer
+    lk.release_read()
+    lk.release_read()
+    w.join(5)
+    t3.join(5)
+    assert got == ["w"] and r3 == [1]
+
+
+def test_coalescer_batches_and_keeps_order():
+    seen = []
+
+    def run(batch):
+        seen.append(list(batch))
+        time.sleep(0.01)
+        return [x * 10 for x in batch]
+
+    c = QueryCoalescer(run, window_s=0.002, max_batch=16)
+    futs = [c.submit(i) for i in range(40)]
+    assert [f.result(5) for f in futs] == [i * 10 for i in range(40)]
+    assert sum(len(b) for b in seen) == 40
+    assert max(len(b) for b in seen) <= 16 and len(seen) < 40
+    assert [x for b in seen for x in b] == list(range(40))  # FIFO
+    c.close()
+
+
+def test_coalescer_propagates_errors_to_the_batch_only():
+    def run(batch):
+        if "bad" in batch:
+            raise ValueError("boom")
+        return batch
+
+    c = QueryCoalescer(run, window_s=0.0)
+    assert c.submit("ok").result(5) == "ok"
+    f = c.submit("bad")
+    with pytest.raises(ValueError):
+        f.result(5)
+    assert c("fine") == "fine"  # the dispatcher survives
+    c.close()
+
+
+def test_coalescer_lone_request_latency():
+    c = QueryCoalescer(lambda b: b, window_s=0.0005)
+    c("warm")
+    t = time.perf_counter()
+    for _ in range(50):
+        c("x")
+    assert (time.perf_counter() - t) / 50 < 0.01
+    c.close()

@@ -56,6 +56,15 @@ class FakeEngine:
         rows += [[5, t, 0, 0, 2] for t in self.tracks if t not in self.removed and len(rows) < 3]
         return [np.array(rows, dtype=np.int64).reshape(-1, 5)]
 
+    def query_pcm(self, clips):
+        if self.fail == "extract":
+            raise _lib.EngineError(-1, "bad input")
+        out = []
+        for c in clips:
+            self._last = [np.asarray(c[:3], dtype=np.float32)]
+            out.append(self.query_extracted()[0])
+        return out
+
     def index_save(self, path):
         blob = json.dumps({"tracks": {str(t): v.tolist() for t, v in self.tracks.items()},
                            "removed": sorted(self.removed)})
@@ -320,3 +329,101 @@ def test_exact_lane_engine_unavailable_returns_empty(tmp_path, monkeypatch):
         assert run(exact.run_exact_lane(PCM, 5)) == []
     finally:
         fp.set_service(None)
+
+
+def _pcm_of(v: float) -> bytes:
+    return np.full(16000, v, dtype="<f4").tobytes()
+
+
+def test_concurrent_queries_coalesced_equal_serial(svc, monkeypatch):
+    """64 concurrent olaf_query coroutines (the reference would spawn 64 olaf_c processes) are served by
+    a few batched engine calls and each gets exactly the rows of a serial call with its PCM."""
+    import time as _t
+
+    names = [uuid.UUID(int=1000 + i) for i in range(8)]
+    for i, n in enumerate(names):
+        assert run(fp.olaf_index_track(_pcm_of(0.1 * (i + 1)), n))
+    serial = {i: svc.query(_pcm_of(0.1 * (i % 8 + 1))) for i in range(8)}
+    eng = svc._eng()
+    slow = eng.query_pcm
+    calls = []
+
+    def slow_query(clips):  # a batch takes 5 ms: later arrivals queue up behind it
+        calls.append(len(clips))
+        _t.sleep(0.005)
+        return slow(clips)
+
+    monkeypatch.setattr(eng, "query_pcm", slow_query)
+
+    async def many():
+        return await asyncio.gather(*[fp.olaf_query(_pcm_of(0.1 * (i % 8 + 1))) for i in range(64)])
+
+    got = run(many())
+    for i, rows in enumerate(got):
+        assert rows == serial[i % 8]
+        assert rows and rows[0].reference_path == str(names[i % 8])
+    assert sum(calls) == 64 and len(calls) < 64 and max(calls) > 1
+
+
+def test_queries_wait_for_writer(svc):
+    """A query submitted while a store holds the write lock runs after it and sees the new track."""
+    import threading
+
+    tid = uuid.UUID(int=77)
+    svc._eng()
+    svc._rw.acquire_write()
+    fut = svc.submit_query(_pcm_of(0.5))
+    t = threading.Thread(target=lambda: None)
+    t.start()
+    t.join()
+    assert not fut.done()
+    # the writer's work, done while holding the lock (index_track would take it itself)
+    eng = svc._engine
+    recs = eng.extract_host([np.full(16000, 0.5, np.float32)])[0]
+    eng.index_add_records(svc._next, recs)
+    svc._apply_store_maps(eng, str(tid), svc._next)
+    svc._next += 1
+    svc._rw.release_write()
+    assert fut.result(timeout=10)[0].reference_path == str(tid)
+
+
+def test_bulk_ingest_recipe(svc, tmp_path):
+    """INTEGRATION.md bulk ingest: persist = False skips the per-track journal, the catalog already on
+    disk is still loaded first, and one checkpoint() commits everything for the next start."""
+    first = uuid.UUID(int=1)
+    assert run(fp.olaf_index_track(_pcm_of(0.9), first))  # an existing catalog (journaled)
+    bulk = fp.FingerprintService(tmp_path / "db")
+    bulk.persist = False
+    names = [uuid.UUID(int=10 + i) for i in range(5)]
+    for i, n in enumerate(names):
+        assert bulk.index_track(_pcm_of(0.2 + 0.1 * i), str(n))
+    jour = tmp_path / "db" / "journal.0.aidfj"
+    size_before = jour.stat().st_size
+    assert jour.stat().st_size == size_before  # nothing journaled during the bulk
+    bulk.checkpoint()
+    bulk.close()
+    again = fp.FingerprintService(tmp_path / "db")
+    assert again.query(_pcm_of(0.9))[0].reference_path == str(first)
+    for i, n in enumerate(names):
+        assert again.query(_pcm_of(0.2 + 0.1 * i))[0].reference_path == str(n)
+
+
+def test_failed_auto_checkpoint_keeps_operation(svc, tmp_path, monkeypatch):
+    """A checkpoint that fails inside the engine (EngineError) after the store was journaled leaves the
+    store successful (True), removes the half-written snapshot and keeps the journal for the restart."""
+    svc.checkpoint_min_bytes = 1
+    svc._eng()
+    svc._store.checkpoint_min_bytes = 1
+    eng = svc._engine
+
+    def bad_save(path):
+        open(path, "w").write("partial")
+        raise _lib.EngineError(-2, "device error while saving")
+
+    monkeypatch.setattr(eng, "index_save", bad_save)
+    tid = uuid.UUID(int=5)
+    assert run(fp.olaf_index_track(_pcm_of(0.3), tid)) is True
+    assert not list((tmp_path / "db").glob("*.tmp"))
+    assert run(fp.olaf_index_track(_pcm_of(0.4), uuid.UUID(int=6))) is True  # backoff: no retry storm
+    again = fp.FingerprintService(tmp_path / "db")
+    assert again.query(_pcm_of(0.3))[0].reference_path == str(tid)

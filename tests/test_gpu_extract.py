@@ -72,6 +72,21 @@ def test_long_track_multi_chunk(gpu_engine):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("order", ["short_first", "short_last", "short_both"])
+def test_frameless_clip_beside_two_chunk_clip(gpu_engine, order):
+    """A clip too short for one frame has no K3 chunk, so [short, two-chunk clip] has as many chunks as
+    clips: K3 must still search the descriptors (not map chunk -> clip) and run its COUNT pass (the
+    second chunk's base). Both clips' hashes equal the oracle's."""
+    short = _clip(71, 1000)
+    two = _clip(72, 2048 + 512 * 1500, start=99, snr=20)  # 1501 frames: 2 chunks of 1024 anchor frames
+    clips = {"short_first": [short, two], "short_last": [two, short], "short_both": [short, two, short]}[order]
+    got = gpu_engine.extract_host(clips)
+    for c, x in enumerate(clips):
+        ref = O.fingerprint(x, HOP)
+        assert np.array_equal(got[c], ref), f"clip {c}: hashes differ"
+    assert sum(len(g) for g in got) > 1000
+
+
 def test_batch_256_full_config(gpu_engine):
     """BASELINE config 2 shape: 256 x 10 s, device-resident PCM, every clip bit-exact."""
     import torch
@@ -256,16 +271,16 @@ def test_band_limited_quarters_bit_exact(gpu_engine):
 
 
 @pytest.mark.parametrize("slots_x", ["1", "1.25", "1.5", "3"])
-def test_k2_strip_multipliers_bit_exact(monkeypatch, slots_x):
+def test_k2_strip_multipliers_bit_exact(slots_x):
     """K2's strip count follows the measured cold-wave fraction (1, 1.25 or 1.5 strips per resident
     workgroup slot, engine.cpp extract_locked; strip-cold waves exit). Every fixed multiplier, including
     one that leaves workgroups waiting for slots, gives the oracle's peaks and hashes bit for bit, on a
     band-limited batch where about half of the quarter waves are strip-cold and exit."""
     from aidfp.engine import Engine
 
-    monkeypatch.setenv("AIDFP_K2_SLOTS_X", slots_x)
     clips = [_clip(t, 44100 * 4 + 313 * t, snr=None if t % 3 else 20) for t in range(24)]
     with Engine(SR) as eng:
+        eng.force("k2_strips_x100", round(float(slots_x) * 100))
         got = eng.extract_host(clips)
         for c, x in enumerate(clips):
             pk = peaks_from_mask(eng.peakmask(c, len(x)))

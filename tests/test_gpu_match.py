@@ -193,8 +193,8 @@ def test_zero_hash_track_has_a_slot():
             eng.index_remove(77)
 
 
-def test_sort_build_equals_atomic_build(monkeypatch):
-    """K4 sort build (index_sort.hip, default) vs the atomic counting sort (AIDFP_K4=atomic): same live
+def test_sort_build_equals_atomic_build():
+    """K4 sort build (index_sort.hip, default) vs the atomic counting sort (force k4_build 2): same live
     postings and identical query rows, with removed tracks (sentinel keys sorted past the live ones)."""
     import torch
 
@@ -205,9 +205,9 @@ def test_sort_build_equals_atomic_build(monkeypatch):
           for i in range(0, 20, 2)]
     out = {}
     for mode in ("atomic", "sort"):
-        monkeypatch.setenv("AIDFP_K4", mode)
         eng = Engine(SR)
         try:
+            eng.force("k4_build", 2 if mode == "atomic" else 1)
             pcm = torch.empty(len(tracks) * n, dtype=torch.float32, device="cuda")
             eng.synth(pcm.data_ptr(), tracks, np.zeros(len(tracks), np.int64), n)
             eng.extract_device(pcm.data_ptr(), np.arange(len(tracks) + 1, dtype=np.int64) * n)

@@ -18,9 +18,7 @@ HOP = 512
 
 @pytest.mark.parametrize("path", ["auto", "lds", "global", "global2"])
 @pytest.mark.parametrize("per_hash", [0, 30, 90, 160])
-def test_rows_equal_oracle_under_load(per_hash, path, monkeypatch):
-    monkeypatch.setenv("AIDFP_K5_PATH", path.rstrip("2"))  # read at engine creation
-    monkeypatch.setenv("AIDFP_K5_PARTS", "2" if path == "global2" else "0")
+def test_rows_equal_oracle_under_load(per_hash, path):
     rng = np.random.default_rng(per_hash)
     track = synth.synth(7, 0, 30 * SR, SR)
     trec = O.fingerprint(track, HOP)
@@ -43,6 +41,8 @@ def test_rows_equal_oracle_under_load(per_hash, path, monkeypatch):
             t.append(((sel >> np.uint64(32)) + np.uint64(100 + k)).astype(np.uint32))
     H, TR, T = (np.ascontiguousarray(np.concatenate(a)) for a in (h, tr, t))
     with Engine(SR) as eng:
+        eng.force("k5_path", {"auto": 0, "lds": 1, "global": 2, "global2": 2}[path])
+        eng.force("k5_parts", 2 if path == "global2" else 0)
         eng.index_add_postings(H.ctypes.data, TR.ctypes.data, T.ctypes.data, len(H), device=False)
         eng.index_finalize()
         post = eng.index_export()

@@ -124,3 +124,13 @@ def test_match_oracle_votes():
     rows = O.query(post, q, min_match=1)
     assert rows[0].tolist() == [3, 7, 100, 0, 2]
     assert sorted(r[1] for r in rows) == [7, 8]
+
+
+def test_numpy_scipy_path_matches_on_synthetic_clips():
+    """The bench's NumPy/SciPy cpu_baseline leg (float64 FFT) gives the spec's records on the synthetic
+    workloads (band-limited and full-band, clean and noisy): its timing is for the same output."""
+    from aidfp import synth
+
+    for tr, snr, fmax in ((3, None, 8000), (4, 20.0, 8000), (5, None, 20000)):
+        x = synth.synth(tr, 0, 44100 * 4, 44100, snr_db=snr, fmax_hz=fmax)
+        assert np.array_equal(O.fingerprint_numpy(x, 512), O.fingerprint(x, 512))
