@@ -48,10 +48,11 @@ void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint
                           const uint8_t *tomb, uint32_t n_tracks, uint32_t *cursor, uint64_t *post, hipStream_t s);
 void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
 size_t index_sort_temp_bytes(int64_t n);
+size_t radix_scratch_u32(int64_t n);
 hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
-                                   uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes,
-                                   uint32_t *cnt, uint64_t **vals_out, hipStream_t s);
+                                   uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
+                                   uint32_t *scratch, uint32_t *cnt, uint64_t **vals_out, hipStream_t s);
 void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
                     uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
                     uint32_t *ot, hipStream_t s);
@@ -158,8 +159,9 @@ struct aid_engine {
     DevBuf<uint64_t> idx_post;
     DevBuf<uint32_t> srt_k0, srt_k1;  // K4 sort build: key double buffer
     DevBuf<uint64_t> srt_v;           // K4 sort build: the value buffer idx_post pairs with
-    DevBuf<uint8_t> srt_tmp;          // K4 sort build: radix-sort temporary storage
-    int k4_mode = 1;                  // aid_engine_force K4_BUILD: 1 = sort build (default), 0 = atomic counting sort
+    DevBuf<uint8_t> srt_tmp;          // K4 rocPRIM build (A/B): its temporary storage
+    DevBuf<uint32_t> srt_scratch;     // K4 radix build: per-tile digit counts, their scan, scan temporary
+    int k4_mode = 2;                  // aid_engine_force K4_BUILD: 2 radix sort (default), 1 rocPRIM sort, 0 atomic
     bool index_built = false, index_dirty = true;
     int64_t n_indexed = 0;
     int64_t n_buckets_used = 0;
@@ -421,6 +423,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->srt_k1.release();
     e->srt_v.release();
     e->srt_tmp.release();
+    e->srt_scratch.release();
     e->nz.release();
     e->q_recs.release();
     e->q_start.release();
@@ -494,8 +497,8 @@ int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
             e->desc_dev_for_key = nullptr;  // strip bases change: rebuild the descriptors
             return AID_OK;
         case AID_FORCE_K4_BUILD:
-            if (value < 0 || value > 2) return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 sort, 2 atomic");
-            e->k4_mode = value == 2 ? 0 : 1;
+            if (value < 0 || value > 3) return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 radix, 2 atomic, 3 rocPRIM");
+            e->k4_mode = value == 2 ? 0 : value == 3 ? 1 : 2;
             e->index_dirty = true;
             return AID_OK;
         default:
@@ -1286,22 +1289,31 @@ static int finalize_locked(aid_engine *e) {
     HIP_TRY(hipMemsetAsync(e->idx_cnt.p, 0, K * sizeof(uint32_t), s));
     HIP_TRY(e->nz.reserve(1));
     HIP_TRY(hipMemsetAsync(e->nz.p, 0, sizeof(unsigned long long), s));
-    if (e->k4_mode == 1 && e->n_post > 0) {
-        // sort build (index_sort.hip): keys + values -> stable radix sort -> bucket lengths -> scan
+    if (e->k4_mode >= 1 && e->n_post > 0) {
+        // sort build (index_sort.hip): stable radix sort of (key27, track | t << 32) -> bucket lengths -> scan
         const size_t np = (size_t)e->n_post;
-        const size_t tb = index_sort_temp_bytes(e->n_post);
-        if (tb == 0) return fail(AID_ERR_DEVICE, "radix sort: temporary storage query failed");
+        const bool rocprim_ab = e->k4_mode == 1;
+        size_t tb = 0;
+        if (rocprim_ab) {
+            tb = index_sort_temp_bytes(e->n_post);
+            if (tb == 0) return fail(AID_ERR_DEVICE, "radix sort: temporary storage query failed");
+            HIP_TRY(e->srt_tmp.reserve(tb));
+        } else {
+            HIP_TRY(e->srt_scratch.reserve(radix_scratch_u32(e->n_post)));
+        }
         HIP_TRY(e->srt_k0.reserve(np));
         HIP_TRY(e->srt_k1.reserve(np));
         HIP_TRY(e->srt_v.reserve(np));
-        HIP_TRY(e->srt_tmp.reserve(tb));
         uint64_t *sorted = nullptr;
-        HIP_TRY(launch_index_sort_build(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks,
-                                        e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
-                                        e->idx_cnt.p, &sorted, s));
-        if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended
-        launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
-        launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
+        {
+            ProfScope ps(e, AID_K_INDEX_BUILD, s);
+            HIP_TRY(launch_index_sort_build(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks,
+                                            e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
+                                            rocprim_ab, e->srt_scratch.p, e->idx_cnt.p, &sorted, s));
+            if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended
+            launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
+            launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
+        }
     } else {
         launch_index_count(e->p_hash.p, e->p_track.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p, s);
         launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
@@ -1321,6 +1333,15 @@ static int finalize_locked(aid_engine *e) {
     e->index_built = true;
     e->index_dirty = false;
     e->tomb_since_build = 0;  // the build skipped every removed track's postings
+    // the sort's double buffers are 16 B per posting (15 GB at the 100k-track catalog): kept for the next build
+    // of a small index (a store + query cycle rebuilds it), released above 1 GiB
+    if ((e->srt_k0.n + e->srt_k1.n) * 4 + e->srt_v.n * 8 + e->srt_tmp.n + e->srt_scratch.n * 4 > ((size_t)1 << 30)) {
+        e->srt_k0.release();
+        e->srt_k1.release();
+        e->srt_v.release();
+        e->srt_tmp.release();
+        e->srt_scratch.release();
+    }
     return AID_OK;
 }
 

@@ -51,7 +51,8 @@ extern "C" {
 #define AID_K_MATCH 5
 #define AID_K_RESAMPLE 6
 #define AID_K_DEDUP 7
-#define AID_K_COUNT 8
+#define AID_K_INDEX_BUILD 8 /* the K4 sort build (sort + bucket lengths + offsets) */
+#define AID_K_COUNT 9
 
 typedef struct aid_engine aid_engine;
 
@@ -94,7 +95,7 @@ int aid_engine_config(const aid_engine *e, aid_config *out);
 #define AID_FORCE_K5_PARTS 2       /* 0 by vote count, else 1, 2 or 4 key partitions per query (K5a) */
 #define AID_FORCE_K5_BATCH 3       /* 0 default (2048), else global-path queries per launch */
 #define AID_FORCE_K2_STRIPS_X100 4 /* 0 adaptive, else 100 x K2 strips per resident workgroup slot */
-#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix-sort build, 2 atomic counting-sort build */
+#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B) */
 int aid_engine_force(aid_engine *e, int32_t what, int32_t value);
 
 /* Frames and worst-case record count of a clip of n samples (FPSPEC 1, 5). */

@@ -194,7 +194,8 @@ def test_zero_hash_track_has_a_slot():
 
 
 def test_sort_build_equals_atomic_build():
-    """K4 sort build (index_sort.hip, default) vs the atomic counting sort (force k4_build 2): same live
+    """K4 hand-written radix-sort build (index_sort.hip, default) vs the atomic counting sort (force k4_build 2)
+    and rocPRIM's sort (3): same live
     postings and identical query rows, with removed tracks (sentinel keys sorted past the live ones)."""
     import torch
 
@@ -204,10 +205,10 @@ def test_sort_build_equals_atomic_build():
     qs = [synth.synth(int(tracks[i]), int(rng.integers(0, 7 * SR)), 5 * SR, SR, snr_db=20.0, salt=40 + i)
           for i in range(0, 20, 2)]
     out = {}
-    for mode in ("atomic", "sort"):
+    for mode in ("atomic", "sort", "rocprim"):
         eng = Engine(SR)
         try:
-            eng.force("k4_build", 2 if mode == "atomic" else 1)
+            eng.force("k4_build", {"atomic": 2, "sort": 1, "rocprim": 3}[mode])
             pcm = torch.empty(len(tracks) * n, dtype=torch.float32, device="cuda")
             eng.synth(pcm.data_ptr(), tracks, np.zeros(len(tracks), np.int64), n)
             eng.extract_device(pcm.data_ptr(), np.arange(len(tracks) + 1, dtype=np.int64) * n)
@@ -219,7 +220,8 @@ def test_sort_build_equals_atomic_build():
             out[mode] = (eng.index_stats(), eng.query(recs))
         finally:
             eng.close()
-    (sa, ra), (ss, rs) = out["atomic"], out["sort"]
+    (sa, ra), (ss, rs), (sr, rr) = out["atomic"], out["sort"], out["rocprim"]
+    assert sr == ss and all(np.array_equal(a, b) for a, b in zip(rr, rs))  # hand-written sort == rocPRIM's
     assert sa["live"] == ss["live"] > 0 and sa["postings"] == ss["postings"]
     assert any(len(r) for r in rs)
     for q, (a, b) in enumerate(zip(ra, rs)):
