@@ -22,9 +22,9 @@ AID_PCM_DEVICE = 1
 AID_FLAG_KEEP_POWER = 1
 AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD = 1, 2, 3, 4, 5
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
-AID_K_COUNT = 9
+AID_K_COUNT = 12
 KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample",
-                "dedup", "index_build"]
+                "dedup", "index_build", "vote_hist", "hot_scan", "vote_final"]
 
 
 class EngineUnavailable(RuntimeError):
@@ -105,6 +105,7 @@ SIGNATURES = [
     ("aid_index_compact", ctypes.c_int, [P, P]),
     ("aid_index_finalize", ctypes.c_int, [P]),
     ("aid_index_stats", ctypes.c_int, [P, P, P, P]),
+    ("aid_match_stats", ctypes.c_int, [P, P, I32, I32]),
     ("aid_index_export", ctypes.c_int, [P, P, P, P, I64, I64, I32]),
     ("aid_comm_id", ctypes.c_int, [P]),
     ("aid_comm_create", ctypes.c_int, [P, P, I32, I32, P]),

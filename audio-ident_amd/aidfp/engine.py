@@ -213,6 +213,13 @@ class Engine:
         check(self._lib.aid_index_stats(self._h, ctypes.byref(n), ctypes.byref(live), ctypes.byref(nt)))
         return {"postings": n.value, "live": live.value, "tracks": nt.value}
 
+    def match_stats(self, reset: bool = False) -> dict:
+        """Cumulative K5 counters (aid_match_stats): queries, votes, postings read, path split, records."""
+        out = np.zeros(6, dtype=np.int64)
+        check(self._lib.aid_match_stats(self._h, _p(out), 6, 1 if reset else 0))
+        return dict(zip(("queries", "votes", "posting_reads", "queries_lds", "queries_global", "records"),
+                        (int(x) for x in out)))
+
     # ---- PCM front-end (FPSPEC 8): downmix + resample, device buffers ----
     def resample_len(self, n: int, sr_in: int, sr_out: int) -> int:
         return int(self._lib.aid_resample_len(int(n), int(sr_in), int(sr_out)))

@@ -64,7 +64,7 @@ void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
-                  int parts, hipStream_t s);
+                  int parts, int stage, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
@@ -213,6 +213,8 @@ struct aid_engine {
     int k5_path = 0;       // aid_engine_force K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int k5_parts = 0;      // aid_engine_force K5_PARTS: K5a key partitions per query (0 = by vote count)
     bool k5_spec_ok = true;  // the previous query batch's heaviest query fitted the LDS path (speculation gate)
+    // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
+    int64_t st_queries = 0, st_votes = 0, st_post_reads = 0, st_q_global = 0, st_q_lds = 0, st_records = 0;
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     size_t k5_batch = 2048;        // global-path queries per launch
     hipStream_t last_stream = nullptr;
@@ -1351,6 +1353,15 @@ int aid_index_finalize(aid_engine *e) {
     return finalize_locked(e);
 }
 
+int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset) {
+    if (!e || (n > 0 && !out)) return fail(AID_ERR_INVALID, "aid_match_stats: bad argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const int64_t v[6] = {e->st_queries, e->st_votes, e->st_post_reads, e->st_q_lds, e->st_q_global, e->st_records};
+    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    if (reset) e->st_queries = e->st_votes = e->st_post_reads = e->st_q_lds = e->st_q_global = e->st_records = 0;
+    return AID_OK;
+}
+
 int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     if (n_postings) *n_postings = e->n_post;
@@ -1690,7 +1701,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     std::vector<int32_t> spec_n;
     if (speculate) {
         {
-            ProfScope ps(e, AID_K_MATCH, s);
+            ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, s);
         }
@@ -1714,6 +1725,13 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     for (int q = 0; q < nq; ++q) vmax = std::max(vmax, h_votes[q]);
     const double votes = (double)vmax;
     e->k5_spec_ok = 2.0 * votes <= 65536.0;
+    e->st_queries += nq;
+    for (int q = 0; q < nq; ++q) {
+        e->st_votes += h_votes[q];
+        e->st_records += h_count[q];
+    }
+    if (speculate)
+        for (int q = 0; q < nq; ++q) e->st_post_reads += h_votes[q];  // the LDS path ran every query once
     // global histogram, sized for the votes that pass K5a's 2^20-bit seen filter (all but the
     // distinct bits: v - m(1 - e^{-v/m})) at ~2 per bucket: a chance bucket reaching
     // min_match - 1 then has probability ~1e-5. Sizing it for ALL votes (2 buckets each: 2 MB rows on
@@ -1736,7 +1754,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // through to the global-histogram path below
     if (fast) {
         {
-            ProfScope ps(e, AID_K_MATCH, s);
+            ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, s);
         }
@@ -1753,8 +1771,13 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         }
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();
+        for (int q = 0; q < nq; ++q) e->st_post_reads += h_votes[q];
+        e->st_q_lds += nq;
     }
+    if (speculate) e->st_q_lds += nq;
     for (int attempt = 1; !todo.empty(); ++attempt, bits += 2) {
+        for (int q : todo) e->st_post_reads += h_votes[q] * (parts + 1);  // K5a once per key partition, K5b once
+        e->st_q_global += (int64_t)todo.size();
         if (bits > 26) return fail(AID_ERR_STATE, "query vote table overflow (too many candidate votes)");
         const size_t H = (size_t)1 << bits;
         const int batch = (int)std::max<size_t>(1, std::min<size_t>(e->k5_batch, ((size_t)4 << 30) / (H * 4)));
@@ -1783,11 +1806,12 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         const int n = (int)order.size();
         for (int q0 = 0; q0 < n; q0 += batch) {
             const int nb = std::min(batch, n - q0);
-            {
-                ProfScope ps(e, AID_K_MATCH, s);
+            // K5a, K5h, K5b, each with its own dispatch-attached events when profiled
+            for (int stage = 1; stage <= 3; ++stage) {
+                ProfScope ps(e, stage == 1 ? AID_K_VOTE_HIST : stage == 2 ? AID_K_HOT_SCAN : AID_K_VOTE_FINAL, s, true);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_hist.p, bits, e->q_hot.p, out_rows + (size_t)q0 * mr * 5,
-                             out_n + q0, e->tomb_since_build > 0, parts, s);
+                             out_n + q0, e->tomb_since_build > 0, parts, stage, s);
             }
             HIP_TRY(hipGetLastError());
         }

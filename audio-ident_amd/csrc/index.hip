@@ -672,7 +672,7 @@ void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
                    tomb_live, nullptr, 1};
-    hipLaunchKernelGGL(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
+    timed_launch(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
 }
 
 void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,
@@ -705,13 +705,15 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
-                  int parts, hipStream_t s) {
+                  int parts, int stage, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
                    nrows, tomb_live, hot, parts};
-    hipLaunchKernelGGL(k_vote_hist, dim3(nq * parts), dim3(1024), 0, s, qp);
-    hipLaunchKernelGGL(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
-    hipLaunchKernelGGL(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
+    // stage = 0: all three kernels; 1, 2, 3: K5a, K5h, K5b alone (the engine times them one by one)
+    if (stage == 0 || stage == 1) timed_launch(k_vote_hist, dim3(nq * parts), dim3(1024), 0, s, qp);
+    if (stage == 0 || stage == 2)
+        timed_launch(k_hot_scan, dim3(16, (unsigned)(nq < 65535 ? nq : 65535)), dim3(256), 0, s, qp);
+    if (stage == 0 || stage == 3) timed_launch(k_vote_final, dim3(nq), dim3(1024), 0, s, qp);
 }
 
 // exact vote count of each query: the sum of its records' bucket lengths (one block per query)

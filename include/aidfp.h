@@ -52,7 +52,10 @@ extern "C" {
 #define AID_K_RESAMPLE 6
 #define AID_K_DEDUP 7
 #define AID_K_INDEX_BUILD 8 /* the K4 sort build (sort + bucket lengths + offsets) */
-#define AID_K_COUNT 9
+#define AID_K_VOTE_HIST 9    /* K5a: seen filter + global vote histogram (global match path) */
+#define AID_K_HOT_SCAN 10    /* K5h: histogram rows -> hot-bucket bitmaps */
+#define AID_K_VOTE_FINAL 11  /* K5b: exact (track, d) table of the hot votes, best d per track, rows */
+#define AID_K_COUNT 12       /* AID_K_MATCH (5) is the LDS match path (k_match_lds) */
 
 typedef struct aid_engine aid_engine;
 
@@ -174,6 +177,11 @@ int aid_index_remove(aid_engine *e, uint32_t track);
  * `olaf_c del` frees its entries). *n_removed = postings dropped. The CSR is rebuilt lazily. */
 int aid_index_compact(aid_engine *e, int64_t *n_removed);
 int aid_index_finalize(aid_engine *e);
+/* Cumulative match counters since the last reset: out[0] queries, [1] exact votes (postings whose hash
+   a query record hits), [2] postings K5 read (LDS path: once per vote; global path: once per key
+   partition in K5a + once in K5b), [3] queries answered on the LDS path, [4] on the global path,
+   [5] query records. The match roofline is 8 B x out[2] / the K5 kernels' time. */
+int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset);
 /* n_postings = stored postings, n_live = postings in the built CSR (-1 if stale), n_tracks = max id + 1 */
 int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks);
 /* Copy stored postings [first, first+count) to host or device columns (RCCL all-gather export). */
