@@ -45,6 +45,12 @@ inline int peak_strip_len(const int64_t *frames, int n, int64_t slots) {
     return (int)lo;
 }
 
+// K1 -> K2 hot word of a power row (u64): bit hot_bit(c) is set when some bin of the 16-bin chunk c
+// (bins 16c .. 16c+15) is > thr. Chunks below 32 map to bit c, the others to bit 95 - c: the order in
+// which K1's lanes hold the mirror bins 1024 - k (stft.hip), so K1 builds the word with two s_quadmask
+// per register and no bit shuffling.
+constexpr int hot_bit(int c) { return c < 32 ? c : 95 - c; }
+
 // K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
 constexpr int kHashChunk = 1024;
 constexpr int kHashChunkPeakCap = 64 * ((kHashChunk + kZoneDT + 7) / 8);

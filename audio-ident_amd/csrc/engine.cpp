@@ -24,10 +24,10 @@
 namespace aid {
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, bool keep_power, hipStream_t s);
+                       uint64_t *hot, float thr, bool keep_power, hipStream_t s);
 int peak_pick_blocks_per_cu();
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
-                      const uint32_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s);
+                      const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s);
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
                       uint64_t *k2_cold_host, uint32_t k2_waves, bool one_chunk_each, hipStream_t s);
@@ -137,7 +137,7 @@ struct aid_engine {
     DevBuf<float> pcm_stage;
     DevBuf<float> power;
     DevBuf<uint64_t> mask;
-    DevBuf<uint32_t> hotw;  // K1 -> K2: per power row, bit b = 64-bin block b has a value > thr
+    DevBuf<uint64_t> hotw;  // K1 -> K2: per power row, bit hot_bit(c) = 16-bin chunk c has a value > thr
     DevBuf<uint32_t> k2_cold;  // K2: strip-cold wave counters (64), summed and reset by K3
     uint64_t *h_cold = nullptr;      // pinned, host-mapped: K3 stores (cold waves | waves << 32) of the last K2 here
     uint64_t *h_cold_dev = nullptr;  // its device address
@@ -1309,7 +1309,10 @@ static int finalize_locked(aid_engine *e) {
         uint64_t *sorted = nullptr;
         {
             ProfScope ps(e, AID_K_INDEX_BUILD, s);
-            HIP_TRY(launch_index_sort_build(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks,
+            bool any_removed = false;
+            for (uint8_t t : e->h_tomb) any_removed = any_removed || t;
+            HIP_TRY(launch_index_sort_build(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post,
+                                            any_removed ? e->tomb.p : nullptr, e->n_tracks,
                                             e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
                                             rocprim_ab, e->srt_scratch.p, e->idx_cnt.p, &sorted, s));
             if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended

@@ -40,9 +40,10 @@ __device__ __forceinline__ uint32_t sort_key26(uint32_t h) {
     return ((h >> 22) << 16) | (((h >> 12) & 0x3FFu) << 6) | (h & 0x3Fu);  // = index.hip key26
 }
 
+// tomb == nullptr: no track is removed (the engine passes none then, saving a dependent load per posting)
 __device__ __forceinline__ uint32_t make_key(uint32_t h, uint32_t tr, const uint8_t *__restrict__ tomb,
                                              uint32_t n_tracks) {
-    return (tr < n_tracks && tomb[tr]) ? (1u << 26) : sort_key26(h);
+    return (tomb && tr < n_tracks && tomb[tr]) ? (1u << 26) : sort_key26(h);
 }
 
 // lanes of the wave holding the same 9-bit digit (among the lanes in `valid`)
@@ -83,8 +84,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
         const int64_t i0 = base + s * 64;
         const uint64_t valid = i0 + 64 <= n ? ~0ull : (i0 >= n ? 0ull : (~0ull >> (64 - (int)(n - i0))));
         const uint64_t m = match_digit(d[s], valid);
-        if (((valid >> lane) & 1) && (m & lanemask_lt(lane)) == 0) c[w][d[s]] += (uint32_t)__popcll(m);
-        asm volatile("" ::: "memory");  // a wave's LDS ops stay in order: the next slot's adds follow
+        // one LDS add per distinct digit of the slot (no return value: the slots' adds issue back to back)
+        if (((valid >> lane) & 1) && (m & lanemask_lt(lane)) == 0) atomicAdd(&c[w][d[s]], (uint32_t)__popcll(m));
     }
     __syncthreads();
     uint32_t t = 0;
@@ -151,20 +152,26 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_scatter(const uint32_t *
         }
     }
     __syncthreads();  // counters zeroed
-    // stable rank inside the wave: slot by slot in item order, lanes in lane order
-    uint32_t rank[kSlots];
+    // stable rank inside the wave: slot by slot in item order, lanes in lane order. The leader of each digit
+    // group adds the group's size to the wave's running counter and gets the count before it (LDS atomics of
+    // one wave are executed in order, so slot s sees slots 0..s-1); the 16 slots' atomics issue back to back,
+    // then each lane takes its leader's value (a cross-lane read) and adds its place in the group
+    uint32_t rank[kSlots], old[kSlots];
+    int lead[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
         const int64_t i0 = base + s * 64;
         const uint64_t valid = i0 + 64 <= n ? ~0ull : (i0 >= n ? 0ull : (~0ull >> (64 - (int)(n - i0))));
         const uint32_t d = (key[s] >> shift) & (kDigits - 1);
         const uint64_t m = match_digit(d, valid);
-        const uint32_t before = cnt[w][d];
-        rank[s] = before + (uint32_t)__popcll(m & lanemask_lt(lane));
-        asm volatile("" ::: "memory");  // every lane's read before the leader's write (in-order LDS)
-        if (((valid >> lane) & 1) && (m & lanemask_lt(lane)) == 0) cnt[w][d] = before + (uint32_t)__popcll(m);
-        asm volatile("" ::: "memory");
+        const uint64_t mine = m | (1ull << lane);  // an invalid lane leads its own (empty) group
+        lead[s] = __ffsll((unsigned long long)mine) - 1;
+        rank[s] = (uint32_t)__popcll(m & lanemask_lt(lane));
+        old[s] = 0;
+        if (((valid >> lane) & 1) && lead[s] == lane) old[s] = atomicAdd(&cnt[w][d], (uint32_t)__popcll(m));
     }
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) rank[s] += (uint32_t)__shfl((int)old[s], lead[s], 64);
     __syncthreads();
     // thread = digit: cross-wave exclusive offsets (in place) and the tile's digit total
     uint32_t tot = 0;

@@ -22,8 +22,8 @@
 //   * a decided row is emitted with 4 wave ballots (one per bin offset i < 4): mask
 //     word 4*w + i of a frame holds, at bit l, the peak flag of bin 256*w + 4*l + i
 //     ("ballot layout"; K3 and aidfp.engine.peaks_from_mask unshuffle it).
-// Only hot 64-bin blocks (K1's per-row hot word) are loaded; a wave whose window blocks are
-// cold in every row of its strip exits at once (it only writes zero mask words).
+// Only hot 16-bin chunks (K1's per-row hot word, aidfp_layout.h hot_bit) are loaded; a wave whose
+// window chunks are cold in every row of its strip exits at once (it only writes zero mask words).
 // Strips are dealt to workgroups XCD-aware so neighbouring strips (which share
 // halo rows) run on the same XCD's L2. The variants measured against this layout
 //  live in the git history (commit c236449, the AID_K2_* switches).
@@ -56,7 +56,7 @@ __device__ __forceinline__ int pkey(float x) {
 // occupancy 4 forced by the launch bounds (<= 128 VGPRs, no spills)
 __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t total_strips, int strip_len, float thr,
-                                                  const uint32_t *__restrict__ hot, uint64_t *__restrict__ mask,
+                                                  const uint64_t *__restrict__ hot, uint64_t *__restrict__ mask,
                                                   uint32_t *__restrict__ cold_cnt) {
     __shared__ __attribute__((aligned(16))) int rows[kRowsPerStep][kBins + 32];  // keys, 16 pads each side
     __shared__ __attribute__((aligned(16))) int bms[kRowsPerStep][256 + 8];  // block maxima, 4 pads each side
@@ -122,22 +122,23 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
     const int rbeg = t0 - kPeakDT;
     const int iters = (t1 - t0) + 2 * kPeakDT;
-    // K1's hot-block word of each row: a thread loads its 4 bins only if their 64-bin block has a
-    // value > thr; others stay 0 (a value <= thr neither is a peak nor suppresses one: exact).
+    // K1's hot word of each row: a thread loads its 4 bins only if their 16-bin chunk has a value
+    // > thr; others stay 0 (a value <= thr neither is a peak nor suppresses one: exact).
     // Words are fetched one step ahead of the row loads they gate (scalar loads)
-    const uint32_t *HW = hot + fb;
-    const int myb = tid >> 4;
-    auto hotword = [&](int r) -> uint32_t { return (r >= 0 && r < F) ? HW[r] : 0u; };
-    // blocks 4w-1 .. 4w+4 hold the wave's bins and their +-15 neighbours
-    const uint32_t wmask = (0x3Fu << (4 * wave)) >> 1;
+    const uint64_t *HW = hot + fb;
+    const int myb = hot_bit(tid >> 2);
+    auto hotword = [&](int r) -> uint64_t { return (r >= 0 && r < F) ? HW[r] : 0ull; };
+    // chunks 16w-1 .. 16w+16 hold the wave's bins and their +-15 neighbours
+    uint64_t wmask = 0;
+    for (int c = max(16 * wave - 1, 0); c <= min(16 * wave + 16, 63); ++c) wmask |= 1ull << hot_bit(c);
     {
         // strip-cold wave: if those blocks are cold in every row the strip reads, every key this wave
         // stages or compares is 0, so it has no candidate and its mask words are 0 (exact, as the
         // per-row cold skip). It writes those zeros, zeroes its staged bins once (the neighbouring
         // waves' windows read them), and only keeps the workgroup's barrier count (2 per 4 rows)
-        uint32_t acc = 0;
-        for (int r = rbeg + lane; r < rbeg + iters; r += 64) acc |= (r >= 0 && r < F) ? HW[r] : 0u;
-        if (__ballot((acc & wmask) != 0u) == 0) {
+        uint64_t acc = 0;
+        for (int r = rbeg + lane; r < rbeg + iters; r += 64) acc |= (r >= 0 && r < F) ? HW[r] : 0ull;
+        if (__ballot((acc & wmask) != 0ull) == 0) {
 #pragma unroll
             for (int j = 0; j < kRowsPerStep; ++j) {
                 reinterpret_cast<int4 *>(&rows[j][16])[tid] = make_int4(0, 0, 0, 0);
@@ -158,14 +159,14 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) {
         const int r = rbeg + j;
-        pf[j] = (j < iters && ((hotword(r) >> myb) & 1u)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
+        pf[j] = (j < iters && ((hotword(r) >> myb) & 1ull)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
                                                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    uint32_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
+    uint64_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) hw[j] = hotword(rbeg + kRowsPerStep + j);
     // hot words of the rows in flight (hsave) and of the rows being processed (hcur)
-    uint32_t hsave[kRowsPerStep], hcur[kRowsPerStep];
+    uint64_t hsave[kRowsPerStep], hcur[kRowsPerStep];
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) hsave[j] = hcur[j] = hotword(rbeg + j);
 
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                     const int rn = rbeg + it + j + kRowsPerStep;
                     hcur[j] = hsave[j];
                     hsave[j] = hw[j];
-                    pf[slot] = (it + j + kRowsPerStep < iters && ((hw[j] >> myb) & 1u))
+                    pf[slot] = (it + j + kRowsPerStep < iters && ((hw[j] >> myb) & 1ull))
                                    ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
                     hw[j] = hotword(rn + kRowsPerStep);
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
 }
 
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
-                      float thr, const uint32_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {
+                      float thr, const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {
     if (total_strips <= 0) return;
     timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
                  strip_len, thr, hot, mask, cold_cnt);

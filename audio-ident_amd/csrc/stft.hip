@@ -55,6 +55,15 @@ static_assert(e1_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave, "E1 regions exc
 
 namespace aid {
 
+// 16-lane groups of a wave-wide mask -> 4 bits: bit g = some lane of lanes 16g .. 16g+15 is set (two
+// s_quadmask_b64: 64 lanes -> 16 quads -> 4 groups of 4 quads)
+__device__ __forceinline__ uint64_t group16(uint64_t m) {
+    uint64_t q, r;
+    asm("s_quadmask_b64 %0, %1" : "=s"(q) : "s"(m));
+    asm("s_quadmask_b64 %0, %1" : "=s"(r) : "s"(q));
+    return r;
+}
+
 // power-row store, non-temporal (streaming): K1 0.268 -> 0.266 ms, K2 0.134 -> 0.130 ms same-box (r02)
 __device__ __forceinline__ void pstore(float *p, float v) {
     __builtin_nontemporal_store(v, p);
@@ -72,7 +81,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
                                                                 int64_t total, int64_t n_waves,
                                                                 const Tables *__restrict__ tab, float *__restrict__ out,
-                                                                uint32_t *__restrict__ hot, float thr, int keep) {
+                                                                uint64_t *__restrict__ hot, float thr, int keep) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
     constexpr int HOP2 = 64 * ROWS;    // hop in float2 units
     __shared__ __attribute__((aligned(16))) float2 lds[kStftWaves][kStftLdsPerWave];  // E1 regions, then E3
@@ -143,7 +152,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     const int nfr = (int)min(f_end - f, clips[lo].frames - t0);
     const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + e1_perm(lane);
     float *dst = out + (clips[lo].frame_base + t0) * kBins;
-    uint32_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
+    uint64_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
 
     float2 ring[16];
 #pragma unroll
@@ -290,7 +299,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                 if constexpr (!LOGMAG) {
                     // straight-line real split: all 16 powers first, then the row's hot word, then the
                     // stores of the hot blocks (scalar branches after the arithmetic, so no branch splits it)
-                    uint32_t hotw = 0;
+                    // the row's hot word (aidfp_layout.h hot_bit): bit of 16-bin chunk c = some bin of c is > thr
+                    uint64_t hotw = 0;
                     float po[8], pm[8];
                     float4 qa, qb;  // the pair of b128 reads that serve bins i and i + 4
 #pragma unroll
@@ -323,12 +333,14 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float xr2 = er - tw.x, xi2 = tw.y - ei;
                         // k = 0 (lane 0, i = 0): the mirror is the dropped Nyquist bin
                         pm[i] = (i == 0 && lane == 0) ? 0.f : __builtin_fmaf(xr2, xr2, xi2 * xi2);
-                        hotw |= __ballot(po[i] > thr) ? 1u << i : 0u;  // bins 64i..64i+63
-                        // lanes 1..63: bins of block 15 - i; lane 0 (i > 0): block 16 - i
-                        const uint64_t hb = __ballot(pm[i] > thr);
-                        // one test marks both blocks: a superset of the hot blocks (exact for K2, which
-                        // only skips blocks marked cold), 3 scalar ops instead of 6 + a 64-bit VALU compare
-                        hotw |= hb ? (i == 0 ? 1u << 15 : 3u << (15 - i)) : 0u;
+                        // direct bins 64i + l: lanes 16g..16g+15 = chunk 4i + g -> bit 4i + g
+                        hotw |= group16(__ballot(po[i] > thr)) << (4 * i);
+                        // mirror bins 1024 - 64i - l: lanes 16g+1 .. 16g+16 = chunk 63 - 4i - g -> bit 32 + 4i + g;
+                        // lane 0 (bin 1024 - 64i, chunk 64 - 4i) -> bit 31 + 4i (lane 0 of register 0 is the
+                        // dropped Nyquist bin, never hot)
+                        const uint64_t hm = __ballot(pm[i] > thr);
+                        hotw |= group16(hm >> 1) << (32 + 4 * i);
+                        if (i > 0) hotw |= (hm & 1ull) << (31 + 4 * i);
                     }
                     {  // bin 512 pairs with itself: every lane computes it (same address, same value),
                        // so its store and the hot word's need no lane-0 branch
@@ -338,22 +350,21 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float xr = er + tw.x, xi = ei + tw.y;
                         const float p512 = __builtin_fmaf(xr, xr, xi * xi);
                         pstore(drow + 512, p512);
-                        hotw |= p512 > thr ? 1u << 8 : 0u;
+                        hotw |= p512 > thr ? 1ull << 63 : 0ull;  // chunk 32
                     }
-                    hotw = __builtin_amdgcn_readfirstlane(hotw);
                     dhot[f] = hotw;
-                    // K2 reads only hot blocks (a value <= thr can neither be a peak nor suppress one, FPSPEC
-                    // 5), so cold blocks are not stored unless the engine keeps the whole plane. Mirror
-                    // store i covers bins 1025-64(i+1) .. 1023-64i of block 15-i (lanes 1..63) and bin
-                    // 1024-64i of block 16-i (lane 0): written when either block is hot
-                    const uint32_t hsel = keep ? 0x1FFFFu : hotw;  // one select, not a branch per store
+                    // K2 reads only hot chunks (a value <= thr can neither be a peak nor suppress one, FPSPEC
+                    // 5), so a store whose chunks are all cold is skipped unless the engine keeps the whole
+                    // plane. Direct store i covers chunks 4i .. 4i+3 (bits 4i..4i+3); mirror store i covers
+                    // chunks 60-4i .. 63-4i (bits 32+4i .. 35+4i) and, by lane 0, chunk 64-4i (bit 31+4i)
+                    const uint64_t hsel = keep ? ~0ull : hotw;  // one select, not a branch per store
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
-                        if ((hsel >> i) & 1u) pstore(drow + lane + 64 * i, po[i]);
+                        if ((hsel >> (4 * i)) & 0xFull) pstore(drow + lane + 64 * i, po[i]);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const uint32_t need = (hsel >> (15 - i)) | (i > 0 ? hsel >> (16 - i) : 0u);
-                        if ((need & 1u) && (i > 0 || lane != 0)) pstore(drow + 1024 - (lane + 64 * i), pm[i]);
+                        const uint64_t need = i > 0 ? (hsel >> (31 + 4 * i)) & 0x1Full : (hsel >> 32) & 0xFull;
+                        if (need && (i > 0 || lane != 0)) pstore(drow + 1024 - (lane + 64 * i), pm[i]);
                     }
                 } else {
                     // log-magnitude rows (aid_spectrogram: the 1e-4 check against float64 numpy), every bin.
@@ -407,7 +418,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 
 template <bool LOGMAG>
 static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
-                        int64_t total, int64_t n_waves, const Tables *tab, float *out, uint32_t *hot, float thr, int keep) {
+                        int64_t total, int64_t n_waves, const Tables *tab, float *out, uint64_t *hot, float thr, int keep) {
     switch (rows) {
         case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
         case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
@@ -421,7 +432,7 @@ static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pc
 // slots = resident K1 waves on the device (CUs x kStftWaves)
 void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
-                       uint32_t *hot, float thr, bool keep_power, hipStream_t s) {
+                       uint64_t *hot, float thr, bool keep_power, hipStream_t s) {
     if (total_frames <= 0) return;
     // one round of equal ranges. A wave reloads its 16-row ring once per segment, so large batches keep
     // >= kStftStrip frames per wave; a batch smaller than that spreads over >= kK1MinFrames-frame ranges
