@@ -1551,7 +1551,12 @@ int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_to
         if (int rc = pack_locked(e, first, e->g_send.p, mx, s)) return rc;
         NCCL_TRY(ncclAllGather(e->g_send.p, e->g_recv.p, 3 * (size_t)mx, ncclUint32, c->comm, s));
         // 3. the union in rank order replaces this rank's shard
-        if (int rc = splice_locked(e, first, e->g_recv.p, W, mx, counts.data(), tracks, s)) return rc;
+        const int rc = splice_locked(e, first, e->g_recv.p, W, mx, counts.data(), tracks, s);
+        // the exchange buffers are (world + 1) x 12 B per largest-shard posting (12 GB at 8 x 12.5k tracks):
+        // scratch of this call only
+        e->g_send.release();
+        e->g_recv.release();
+        if (rc) return rc;
     } else if (int rc = ensure_tracks(e, tracks, s)) {
         return rc;
     }
