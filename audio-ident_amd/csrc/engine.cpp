@@ -52,7 +52,8 @@ size_t radix_scratch_u32(int64_t n);
 hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
                                    uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
-                                   uint32_t *scratch, uint32_t *cnt, uint64_t **vals_out, hipStream_t s);
+                                   uint32_t *scratch, uint32_t *E, uint32_t *offsets, unsigned long long *nz,
+                                   uint64_t **vals_out, hipStream_t s);
 void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
                     uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
                     uint32_t *ot, hipStream_t s);
@@ -1292,7 +1293,7 @@ static int finalize_locked(aid_engine *e) {
     HIP_TRY(e->nz.reserve(1));
     HIP_TRY(hipMemsetAsync(e->nz.p, 0, sizeof(unsigned long long), s));
     if (e->k4_mode >= 1 && e->n_post > 0) {
-        // sort build (index_sort.hip): stable radix sort of (key27, track | t << 32) -> bucket lengths -> scan
+        // sort build (index_sort.hip): stable radix sort of (key27, track | t << 32) -> run ends -> max-scan
         const size_t np = (size_t)e->n_post;
         const bool rocprim_ab = e->k4_mode == 1;
         size_t tb = 0;
@@ -1300,9 +1301,8 @@ static int finalize_locked(aid_engine *e) {
             tb = index_sort_temp_bytes(e->n_post);
             if (tb == 0) return fail(AID_ERR_DEVICE, "radix sort: temporary storage query failed");
             HIP_TRY(e->srt_tmp.reserve(tb));
-        } else {
-            HIP_TRY(e->srt_scratch.reserve(radix_scratch_u32(e->n_post)));
         }
+        HIP_TRY(e->srt_scratch.reserve(radix_scratch_u32(e->n_post)));
         HIP_TRY(e->srt_k0.reserve(np));
         HIP_TRY(e->srt_k1.reserve(np));
         HIP_TRY(e->srt_v.reserve(np));
@@ -1314,10 +1314,9 @@ static int finalize_locked(aid_engine *e) {
             HIP_TRY(launch_index_sort_build(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post,
                                             any_removed ? e->tomb.p : nullptr, e->n_tracks,
                                             e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
-                                            rocprim_ab, e->srt_scratch.p, e->idx_cnt.p, &sorted, s));
+                                            rocprim_ab, e->srt_scratch.p, e->idx_cnt.p, e->idx_off.p, e->nz.p, &sorted,
+                                            s));
             if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended
-            launch_count_nonzero(e->idx_cnt.p, (int64_t)K, e->nz.p, s);
-            launch_scan(e->idx_cnt.p, e->idx_off.p, (int64_t)K, e->scan_tmp.p, s);
         }
     } else {
         launch_index_count(e->p_hash.p, e->p_track.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p, s);

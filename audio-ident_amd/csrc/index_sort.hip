@@ -7,18 +7,20 @@
 // (it sorts past every live key and is dropped), stably, so a bucket keeps arrival order.
 //
 // Hand-written sort (3 passes of 9-bit digits over bits 0..26, 512 digits per pass):
-//   count    per tile of kTile = 8192 postings, the digit histogram (wave ballot-match, then one LDS
-//            add per distinct digit per wave) -> counts[digit][tile];
+//   count    per tile of kTile = 4096 postings, the digit histogram (LDS atomics) -> counts[digit][tile];
 //   scan     exclusive scan of counts in digit-major order: the global start of (digit, tile);
-//   scatter  a workgroup of 8 waves loads its tile (wave w: items w*1024 .. +1023, 64 consecutive per
+//   scatter  a workgroup of 4 waves loads its tile (wave w: items w*1024 .. +1023, 64 consecutive per
 //            load), ranks every item stably inside the tile (ballot match per 64-item slot, wave-private
-//            running digit counters, cross-wave offsets), stages the tile in LDS in sorted order (96 KB)
-//            and writes it out in runs of consecutive positions per digit (coalesced).
-// Pass 1 reads the SoA postings (hash, track, t) and the tombstones itself (key generation fused in);
-// pass 3 writes the values straight into the CSR's post array. Bytes per posting: 8 (count 1) + 24
-// (scatter 1) + 2 x (4 + 24) + 4 (runs) = 92, against ~125 for the rocPRIM build.
-// After the sort, bucket lengths come from the sorted keys (2 atomics per distinct key, in key order),
-// then index.hip's scan gives the offsets.
+//            running digit counters by LDS atomics issued back to back, cross-wave offsets), stages the tile
+//            in LDS in sorted order (48 KB: two workgroups per CU overlap one's loads with the other's
+//            ranking) and writes it out in runs of consecutive positions per digit.
+// Pass 1 reads the SoA postings (hash, track, t) itself (key generation fused in; the tombstones only when a
+// track is removed); pass 3 writes the values straight into the CSR's post array.
+// CSR offsets straight from the sorted keys: at the last posting i of each key's run, E[key + 1] = i + 1;
+// an inclusive max-scan of E over the 2^26 + 1 keys is offsets[] (an absent key inherits the end of the
+// largest key below it). No bucket-length atomics, no separate count of non-empty buckets.
+// Bytes per posting: 8 (count 1) + 24 (scatter 1) + 2 x (4 + 24) + 4 (run ends) = 92, against ~125 for the
+// rocPRIM build.
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "aidfp_device.h"
@@ -29,11 +31,11 @@ constexpr int kSortKeyBits = 27;  // key26 plus the removed-posting sentinel 2^2
 constexpr int kDigitBits = 9;
 constexpr int kDigits = 1 << kDigitBits;
 constexpr int kSortPasses = 3;
-constexpr int kSortThreads = 512;  // 8 waves
+constexpr int kSortThreads = 256;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kSlots = 16;                      // 64-item slots per wave
-constexpr int kTile = kSortThreads * kSlots;    // 8192 postings per tile
-static_assert(kDigits == kSortThreads, "one digit per thread in the tile-level steps");
+constexpr int kTile = kSortThreads * kSlots;    // 4096 postings per tile
+constexpr int kDigitsPerThread = kDigits / kSortThreads;
 static_assert(kDigitBits * kSortPasses == kSortKeyBits, "passes cover the key");
 
 __device__ __forceinline__ uint32_t sort_key26(uint32_t h) {
@@ -59,60 +61,43 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid) {
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// counts[d * tiles + tile] = items of tile `tile` whose digit at `shift` is d
+__device__ __forceinline__ uint64_t valid_lanes(int64_t i0, int64_t n) {
+    return i0 + 64 <= n ? ~0ull : (i0 >= n ? 0ull : (~0ull >> (64 - (int)(n - i0))));
+}
+
+// counts[d * tiles + tile] = items of tile `tile` whose digit at `shift` is d (order does not matter here:
+// one LDS atomic per item)
 template <bool FIRST>
 __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__restrict__ keys,
                                                               const uint32_t *__restrict__ ptrack,
                                                               const uint8_t *__restrict__ tomb, uint32_t n_tracks,
                                                               int64_t n, int shift, uint32_t *__restrict__ counts,
                                                               int64_t tiles) {
-    __shared__ uint32_t c[kSortWaves][kDigits];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int i = tid; i < kSortWaves * kDigits; i += kSortThreads) (&c[0][0])[i] = 0u;
+    __shared__ uint32_t c[kDigits];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kDigits; i += kSortThreads) c[i] = 0u;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)w * (kSlots * 64);
+    const int64_t base = (int64_t)blockIdx.x * kTile;
     uint32_t d[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {  // all loads first
-        const int64_t i = base + s * 64 + lane;
-        uint32_t k = 0;
-        if (i < n) k = FIRST ? make_key(keys[i], ptrack[i], tomb, n_tracks) : keys[i];
-        d[s] = (k >> shift) & (kDigits - 1);
+        const int64_t i = base + s * kSortThreads + tid;
+        d[s] = 0xFFFFFFFFu;
+        if (i < n) d[s] = ((FIRST ? make_key(keys[i], ptrack[i], tomb, n_tracks) : keys[i]) >> shift) & (kDigits - 1);
     }
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
-        const int64_t i0 = base + s * 64;
-        const uint64_t valid = i0 + 64 <= n ? ~0ull : (i0 >= n ? 0ull : (~0ull >> (64 - (int)(n - i0))));
-        const uint64_t m = match_digit(d[s], valid);
-        // one LDS add per distinct digit of the slot (no return value: the slots' adds issue back to back)
-        if (((valid >> lane) & 1) && (m & lanemask_lt(lane)) == 0) atomicAdd(&c[w][d[s]], (uint32_t)__popcll(m));
-    }
+    for (int s = 0; s < kSlots; ++s)
+        if (d[s] != 0xFFFFFFFFu) atomicAdd(&c[d[s]], 1u);
     __syncthreads();
-    uint32_t t = 0;
 #pragma unroll
-    for (int ww = 0; ww < kSortWaves; ++ww) t += c[ww][tid];
-    counts[(int64_t)tid * tiles + blockIdx.x] = t;
-}
-
-// exclusive scan over the 512 threads of the block (wave shuffles + one exchange of the wave totals)
-__device__ __forceinline__ uint32_t block_scan512(uint32_t v, uint32_t *tmp /*[kSortWaves]*/) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
+    for (int j = 0; j < kDigitsPerThread; ++j) {
+        const int dd = tid + j * kSortThreads;
+        counts[(int64_t)dd * tiles + blockIdx.x] = c[dd];
     }
-    if (lane == 63) tmp[w] = x;
-    __syncthreads();
-    uint32_t b = 0;
-#pragma unroll
-    for (int i = 0; i < kSortWaves; ++i) b += i < w ? tmp[i] : 0u;
-    return b + x - v;
 }
 
 template <bool FIRST, bool LAST>
-__global__ __launch_bounds__(kSortThreads) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
+__global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
                                                                 const uint64_t *__restrict__ vals_in,
                                                                 const uint32_t *__restrict__ ptrack,
                                                                 const uint32_t *__restrict__ pt,
@@ -126,12 +111,16 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_scatter(const uint32_t *
     __shared__ uint32_t cnt[kSortWaves][kDigits];  // running per-wave counters, then cross-wave offsets
     __shared__ uint32_t t_start[kDigits];          // first local position of each digit in the tile
     __shared__ uint32_t g_start[kDigits];          // global position of (digit, tile)
-    __shared__ uint32_t tmp[kSortWaves];
+    __shared__ uint32_t wsum[kSortWaves];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t tile0 = (int64_t)blockIdx.x * kTile;
     const int64_t base = tile0 + (int64_t)w * (kSlots * 64);
     for (int i = tid; i < kSortWaves * kDigits; i += kSortThreads) (&cnt[0][0])[i] = 0u;
-    g_start[tid] = offs[(int64_t)tid * tiles + blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kDigitsPerThread; ++j) {
+        const int dd = tid + j * kSortThreads;
+        g_start[dd] = offs[(int64_t)dd * tiles + blockIdx.x];
+    }
     uint32_t key[kSlots];
     uint64_t val[kSlots];
 #pragma unroll
@@ -160,8 +149,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_scatter(const uint32_t *
     int lead[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
-        const int64_t i0 = base + s * 64;
-        const uint64_t valid = i0 + 64 <= n ? ~0ull : (i0 >= n ? 0ull : (~0ull >> (64 - (int)(n - i0))));
+        const uint64_t valid = valid_lanes(base + s * 64, n);
         const uint32_t d = (key[s] >> shift) & (kDigits - 1);
         const uint64_t m = match_digit(d, valid);
         const uint64_t mine = m | (1ull << lane);  // an invalid lane leads its own (empty) group
@@ -173,16 +161,40 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_scatter(const uint32_t *
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) rank[s] += (uint32_t)__shfl((int)old[s], lead[s], 64);
     __syncthreads();
-    // thread = digit: cross-wave exclusive offsets (in place) and the tile's digit total
-    uint32_t tot = 0;
+    // thread = 2 consecutive digits: cross-wave exclusive offsets (in place) and the tile's digit totals, then
+    // the exclusive scan of the totals over the digits (the thread's pair, wave shuffles, wave totals)
+    uint32_t tot[kDigitsPerThread];
 #pragma unroll
-    for (int ww = 0; ww < kSortWaves; ++ww) {
-        const uint32_t c = cnt[ww][tid];
-        cnt[ww][tid] = tot;
-        tot += c;
+    for (int j = 0; j < kDigitsPerThread; ++j) {
+        const int dd = tid * kDigitsPerThread + j;
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < kSortWaves; ++ww) {
+            const uint32_t c = cnt[ww][dd];
+            cnt[ww][dd] = t;
+            t += c;
+        }
+        tot[j] = t;
     }
-    const uint32_t start = block_scan512(tot, tmp);
-    t_start[tid] = start;
+    uint32_t mysum = 0;
+#pragma unroll
+    for (int j = 0; j < kDigitsPerThread; ++j) mysum += tot[j];
+    uint32_t x = mysum;  // inclusive scan over the wave
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t start = x - mysum;
+#pragma unroll
+    for (int i = 0; i < kSortWaves; ++i) start += i < w ? wsum[i] : 0u;
+#pragma unroll
+    for (int j = 0; j < kDigitsPerThread; ++j) {
+        t_start[tid * kDigitsPerThread + j] = start;
+        start += tot[j];
+    }
     __syncthreads();
     // stage the tile in LDS in sorted (digit, item) order
 #pragma unroll
@@ -211,14 +223,102 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_scatter(const uint32_t *
     }
 }
 
-// cnt[k] (zeroed) += run length of key k < 2^26 in the sorted keys: -start at a run's first
-// element, +end+1 at its last (u32 wrap-around; both land before the scan reads cnt)
-__global__ void k_sort_runs(const uint32_t *__restrict__ keys, int64_t n, uint32_t *__restrict__ cnt) {
+// E[key + 1] = i + 1 at the last posting i of each live key's run (E zeroed by the caller); nz += number of
+// live keys (one atomic per workgroup)
+__global__ __launch_bounds__(256) void k_run_ends(const uint32_t *__restrict__ keys, int64_t n,
+                                                  uint32_t *__restrict__ E, unsigned long long *__restrict__ nz) {
+    __shared__ unsigned long long part[4];
+    unsigned long long c = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t k = keys[i];
-        if (k >= (1u << 26)) continue;
-        if (i == 0 || keys[i - 1] != k) atomicAdd(&cnt[k], (uint32_t)(-(uint32_t)i));
-        if (i == n - 1 || keys[i + 1] != k) atomicAdd(&cnt[k], (uint32_t)(i + 1));
+        if (k < (1u << 26) && (i == n - 1 || keys[i + 1] != k)) {
+            E[k + 1] = (uint32_t)(i + 1);
+            ++c;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(nz, part[0] + part[1] + part[2] + part[3]);
+}
+
+// ---- scans over u32 (8 items per thread, wave shuffles): exclusive sum (tile counts) and inclusive max
+// (offsets from run ends). Level 1 per 8192-item block; the block totals are scanned recursively and folded
+// back into every block.
+constexpr int kScanThreads = 1024, kScanItems = 8, kScanBlock = kScanThreads * kScanItems;
+
+template <bool MAX>
+__device__ __forceinline__ uint32_t sop(uint32_t a, uint32_t b) { return MAX ? max(a, b) : a + b; }
+
+template <bool MAX>
+__global__ __launch_bounds__(kScanThreads) void k_scan8(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                       int64_t n, uint32_t *__restrict__ bsum) {
+    __shared__ uint32_t ws[kScanThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t i0 = (int64_t)blockIdx.x * kScanBlock + (int64_t)tid * kScanItems;
+    uint32_t v[kScanItems];
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) v[j] = i0 + j < n ? in[i0 + j] : 0u;
+    uint32_t incl[kScanItems];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) incl[j] = acc = sop<MAX>(acc, v[j]);
+    uint32_t x = acc;  // inclusive over the wave's threads
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x = sop<MAX>(x, y);
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t pre = __shfl_up(x, 1, 64);  // over the threads before this one in the wave
+    if (lane == 0) pre = 0;
+    for (int i = 0; i < w; ++i) pre = sop<MAX>(pre, ws[i]);
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j)
+        if (i0 + j < n) out[i0 + j] = MAX ? sop<MAX>(pre, incl[j]) : pre + incl[j] - v[j];
+    if (tid == kScanThreads - 1) {
+        uint32_t t = 0;
+        for (int i = 0; i < kScanThreads / 64; ++i) t = sop<MAX>(t, ws[i]);
+        bsum[blockIdx.x] = t;
+    }
+}
+
+// out[block b + 1] op= add[b] (the caller offsets `out` by one block when `add` is an inclusive scan)
+template <bool MAX>
+__global__ __launch_bounds__(kScanThreads) void k_scan8_add(uint32_t *__restrict__ out, int64_t n,
+                                                           const uint32_t *__restrict__ add) {
+    const uint32_t a = add[blockIdx.x];
+    const int64_t i0 = (int64_t)blockIdx.x * kScanBlock;
+    for (int j = threadIdx.x; j < kScanBlock; j += kScanThreads)
+        if (i0 + j < n) out[i0 + j] = sop<MAX>(a, out[i0 + j]);
+}
+
+// scratch u32 a scan of n needs (its block totals and their scan, recursively)
+static size_t scan8_tmp(int64_t n) {
+    size_t t = 8;
+    for (int64_t m = n; m > kScanBlock;) {
+        m = (m + kScanBlock - 1) / kScanBlock;
+        t += 2 * (size_t)m + 8;
+    }
+    return t;
+}
+
+// MAX = false: exclusive sum; MAX = true: inclusive max
+template <bool MAX>
+static void scan8(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    uint32_t *bsum = tmp, *boff = tmp + nb;
+    hipLaunchKernelGGL(k_scan8<MAX>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, out, n, bsum);
+    if (nb > 1) {
+        scan8<MAX>(bsum, boff, nb, tmp + 2 * nb + 8, s);
+        if (MAX)  // boff = inclusive max of the block maxima: block b + 1 takes boff[b]
+            hipLaunchKernelGGL(k_scan8_add<MAX>, dim3((unsigned)(nb - 1)), dim3(kScanThreads), 0, s, out + kScanBlock,
+                               n - kScanBlock, (const uint32_t *)boff);
+        else      // boff = exclusive sum of the block totals: block b takes boff[b]
+            hipLaunchKernelGGL(k_scan8_add<MAX>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, out, n,
+                               (const uint32_t *)boff);
     }
 }
 
@@ -233,14 +333,12 @@ __global__ void k_sort_keys(const uint32_t *__restrict__ ph, const uint32_t *__r
     }
 }
 
-void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
-
 int64_t radix_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 
-// scratch of the hand-written sort in u32 units: counts + offsets matrices and the scan's temporary
+// scratch of the sort build in u32 units: the tile counts, their scan, and the scans' temporaries
 size_t radix_scratch_u32(int64_t n) {
     const int64_t c = (int64_t)kDigits * radix_tiles(n);
-    return (size_t)(2 * c + 4 * (c / 1024 + 2) + 4096);
+    return (size_t)(2 * c) + std::max(scan8_tmp(c), scan8_tmp((int64_t)(1u << 26) + 1)) + 64;
 }
 
 // temporary storage of the rocPRIM sort for n pairs
@@ -252,18 +350,23 @@ size_t index_sort_temp_bytes(int64_t n) {
     return bytes;
 }
 
-// keys0/keys1: n u32 each; vals0/vals1: n u64 each (the sorted values end in *vals_out, one of the two);
-// cnt: 2^26 + 1 u32, zeroed by the caller. use_rocprim: the A/B reference (temp/temp_bytes its storage);
-// otherwise `scratch` holds radix_scratch_u32(n) u32.
+// keys0/keys1: n u32 each; vals0/vals1: n u64 each (the sorted values end in *vals_out, one of the two).
+// E (2^26 + 1 u32, zeroed by the caller) receives the run ends, offsets the CSR offsets, *nz (zeroed) the
+// number of live keys. use_rocprim: the A/B reference (temp/temp_bytes its storage); `scratch` holds
+// radix_scratch_u32(n) u32 either way (the offsets scan uses it too).
 hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
                                    uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
-                                   uint32_t *scratch, uint32_t *cnt, uint64_t **vals_out, hipStream_t s) {
+                                   uint32_t *scratch, uint32_t *E, uint32_t *offsets, unsigned long long *nz,
+                                   uint64_t **vals_out, hipStream_t s) {
     *vals_out = vals0;
-    if (n <= 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
+    const int64_t K = (int64_t)(1u << 26) + 1;
+    const int64_t tiles = radix_tiles(n);
+    const int64_t c = (int64_t)kDigits * tiles;
+    uint32_t *stmp = scratch + 2 * c;
     const uint32_t *sorted_keys = nullptr;
-    if (use_rocprim) {
+    if (n > 0 && use_rocprim) {
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_sort_keys, dim3((unsigned)blocks), dim3(256), 0, s, ph, ptrack, pt, n, tomb, n_tracks,
                            keys0, vals0);
         rocprim::double_buffer<uint32_t> k(keys0, keys1);
@@ -273,32 +376,34 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
         if (err != hipSuccess) return err;
         sorted_keys = k.current();
         *vals_out = v.current();
-    } else {
-        const int64_t tiles = radix_tiles(n);
-        const int64_t c = (int64_t)kDigits * tiles;
-        uint32_t *counts = scratch, *offs = scratch + c, *stmp = scratch + 2 * c;
+    } else if (n > 0) {
+        uint32_t *counts = scratch, *offs = scratch + c;
         // pass 1: SoA postings -> (keys1, vals1); pass 2: -> (keys0, vals0); pass 3: -> (keys1, vals1)
         const dim3 g((unsigned)tiles), b(kSortThreads);
         timed_launch(k_radix_count<true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
-        launch_scan(counts, offs, c, stmp, s);
+        scan8<false>(counts, offs, c, stmp, s);
         timed_launch(k_radix_scatter<true, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt, tomb,
                      n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
-        launch_scan(counts, offs, c, stmp, s);
+        scan8<false>(counts, offs, c, stmp, s);
         timed_launch(k_radix_scatter<false, false>, g, b, 0, s, (const uint32_t *)keys1, (const uint64_t *)vals1,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
                      kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys0, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, counts, tiles);
-        launch_scan(counts, offs, c, stmp, s);
+        scan8<false>(counts, offs, c, stmp, s);
         timed_launch(k_radix_scatter<false, true>, g, b, 0, s, (const uint32_t *)keys0, (const uint64_t *)vals0,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
                      2 * kDigitBits, (const uint32_t *)offs, tiles, keys1, vals1);
         sorted_keys = keys1;
         *vals_out = vals1;
     }
-    hipLaunchKernelGGL(k_sort_runs, dim3((unsigned)blocks), dim3(256), 0, s, sorted_keys, n, cnt);
+    if (n > 0) {
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
+        hipLaunchKernelGGL(k_run_ends, dim3((unsigned)blocks), dim3(256), 0, s, sorted_keys, n, E, nz);
+    }
+    scan8<true>(E, offsets, K, stmp, s);
     return hipGetLastError();
 }
 

@@ -157,6 +157,10 @@ CATEGORIES = {
     "gain-12dB": dict(snr=20.0, gain=10 ** (-12 / 20), band=None),
     "gain-24dB": dict(snr=20.0, gain=10 ** (-24 / 20), band=None),
     "phone": dict(snr=20.0, gain=1.0, band=(300.0, 3400.0)),
+    # harsher stand-ins for the reference's "mic" / "browser" recordings (quiet, noisy, band-limited)
+    "snr0": dict(snr=0.0, gain=1.0, band=None),
+    "mic-like": dict(snr=5.0, gain=10 ** (-18 / 20), band=(100.0, 7000.0)),
+    "browser-like": dict(snr=10.0, gain=10 ** (-6 / 20), band=(300.0, 7000.0)),
 }
 
 
