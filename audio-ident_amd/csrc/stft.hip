@@ -88,10 +88,11 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     // tables as float4 pairs [h][lane], one ds_read_b128 per pair (hipcc would otherwise merge the
     // stride-512-B float2 reads into ds_read2st64_b64, which costs the LDS twice the cycles):
     //   s_win4[h] = window of rows 2h, 2h+1 ; s_ta4[h] = T1K[lane*k1], k1 = 2h, 2h+1
-    //   s_tb4[h] = T64[(lane&3)*j1], j1 = 2h, 2h+1 ; s_t2[k] = T2K[k], k < 512 (T2K[1024-k] = (-re, im),
-    //   checked in aid_engine_create)
+    //   s_tb4[h] = T64[(lane&3)*j1], j1 = 2h, 2h+1 ; s_t24[j][lane] = T2K[k], T2K[k + 256], k = 64 j + lane < 256:
+    //   the pair the real split uses together (T2K[1024-k] = (-re, im), checked in aid_engine_create; as float2
+    //   reads hipcc merged them into ds_read2st64_b64, 8 LDS cycles per pair instead of 4)
     __shared__ float4 s_win4[512], s_ta4[512];
-    __shared__ float2 s_t2[512];
+    __shared__ float4 s_t24[256];
     __shared__ float4 s_tb4[32];  // [h][lane & 3]: T64[m2*j1] depends on the lane only through m2
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: scalar strip/segment math
@@ -127,8 +128,10 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
             const float2 tb0 = tab->t64[l * a], tb1 = tab->t64[l * b];
             s_tb4[4 * h + l] = make_float4(tb0.x, tb0.y, tb1.x, tb1.y);
         }
-        const int k = l + 64 * h;
-        s_t2[i] = tab->t2k[k];
+        if (i < 256) {
+            const float2 ta = tab->t2k[i], tb = tab->t2k[i + 256];
+            s_t24[i] = make_float4(ta.x, ta.y, tb.x, tb.y);
+        }
     }
     const float2 t512 = tab->t2k[512];
     float2 t16[10];
@@ -302,15 +305,16 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     // the row's hot word (aidfp_layout.h hot_bit): bit of 16-bin chunk c = some bin of c is > thr
                     uint64_t hotw = 0;
                     float po[8], pm[8];
-                    float4 qa, qb;  // the pair of b128 reads that serve bins i and i + 4
+                    float4 qa, qb, t2p;  // the b128 reads that serve bins i and i + 4
 #pragma unroll
                     for (int ii = 0; ii < 8; ++ii) {
-                        // order i = 0, 4, 1, 5, ...: one pair of reads serves two mirror pairs, then dies
+                        // order i = 0, 4, 1, 5, ...: one set of reads serves two mirror pairs, then dies
                         const int i = (ii >> 1) + 4 * (ii & 1);
                         if ((ii & 1) == 0) {
                             const float4 *buf4 = reinterpret_cast<const float4 *>(buf);
                             qa = buf4[e3qa + 128 * (ii >> 1)];
                             qb = buf4[e3qb - 128 * (ii >> 1)];
+                            t2p = s_t24[64 * (ii >> 1) + lane];
                         }
                         // i < 4: a = Z[k], bs = -Z[1024 - k] (stored); i >= 4: a = -Z[k], bs = -Z[1024 - k] (k >= 256)
                         const float2 a = i < 4 ? make_float2(qa.x, qa.y) : make_float2(qa.z, qa.w);
@@ -319,8 +323,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float2 b = i == 0 ? (lane == 0 ? a : make_float2(-bs.x, -bs.y)) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
                         const float er = a.x + b.x, ei = a.y - b.y;
                         const float orr = a.y + b.y, oi = b.x - a.x;
-                        const float2 t2h = s_t2[64 * i + lane];
-                        const float2 tw = cmul(make_float2(orr, oi), make_float2(t2h.x, t2h.y));
+                        const float2 t2h = i < 4 ? make_float2(t2p.x, t2p.y) : make_float2(t2p.z, t2p.w);
+                        const float2 tw = cmul(make_float2(orr, oi), t2h);
                         const float xr = er + tw.x, xi = ei + tw.y;
                         // FPSPEC 4: P = fma(..) * 0.25f. The plane stores Q = fma(..) = 4P instead (one VALU
                         // less per bin): the scaling by 4 is exact and order-preserving, so every decision
@@ -384,7 +388,8 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         const float2 b = i == 0 ? make_float2(bs.x * s0, bs.y * s0) : i < 4 ? make_float2(-bs.x, -bs.y) : bs;
                         const float er = a.x + b.x, ei = a.y - b.y;
                         const float orr = a.y + b.y, oi = b.x - a.x;
-                        const float2 t2h = s_t2[64 * i + lane];
+                        const float4 t2q = s_t24[64 * (i & 3) + lane];
+                        const float2 t2h = i < 4 ? make_float2(t2q.x, t2q.y) : make_float2(t2q.z, t2q.w);
                         const float4 t2 = make_float4(t2h.x, t2h.y, -t2h.x, t2h.y);  // T2K[1024-k] = (-re, im)
                         {
                             const float2 tw = cmul(make_float2(orr, oi), make_float2(t2.x, t2.y));
