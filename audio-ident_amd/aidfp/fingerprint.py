@@ -212,7 +212,8 @@ class FingerprintService:
 
     @staticmethod
     def _pcm(buf: bytes) -> np.ndarray:
-        return np.frombuffer(buf[: len(buf) // 4 * 4], dtype="<f4").astype(np.float32)
+        # a read-only float32 view of the request bytes (no copy; the engine call copies once into its batch)
+        return np.frombuffer(buf, dtype="<f4", count=len(buf) // 4).astype(np.float32, copy=False)
 
     # -- operations (blocking; call from a worker thread) --
     def index_track(self, pcm: bytes, name: str) -> bool:

@@ -59,6 +59,14 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid) {
     return m;
 }
 
+// the tile of workgroup b: consecutive tiles on one XCD (workgroups b and b + 8 share an XCD's L2), so the partial
+// 128-B lines where adjacent tiles' runs of one digit meet -- in the scatter's output and in the digit-major count
+// matrix -- are completed in that L2 instead of going to HBM as separate partial writes and reads
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
+    const int64_t per = nb / 8, rem = nb % 8, x = b % 8, y = b / 8;
+    return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
 __device__ __forceinline__ uint64_t valid_lanes(int64_t i0, int64_t n) {
@@ -77,7 +85,8 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
     const int tid = threadIdx.x;
     for (int i = tid; i < kDigits; i += kSortThreads) c[i] = 0u;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int64_t base = tile * kTile;
     uint32_t d[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {  // all loads first
@@ -92,7 +101,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
 #pragma unroll
     for (int j = 0; j < kDigitsPerThread; ++j) {
         const int dd = tid + j * kSortThreads;
-        counts[(int64_t)dd * tiles + blockIdx.x] = c[dd];
+        counts[(int64_t)dd * tiles + tile] = c[dd];
     }
 }
 
@@ -113,13 +122,14 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
     __shared__ uint32_t g_start[kDigits];          // global position of (digit, tile)
     __shared__ uint32_t wsum[kSortWaves];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t tile0 = (int64_t)blockIdx.x * kTile;
+    const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int64_t tile0 = tile * kTile;
     const int64_t base = tile0 + (int64_t)w * (kSlots * 64);
     for (int i = tid; i < kSortWaves * kDigits; i += kSortThreads) (&cnt[0][0])[i] = 0u;
 #pragma unroll
     for (int j = 0; j < kDigitsPerThread; ++j) {
         const int dd = tid + j * kSortThreads;
-        g_start[dd] = offs[(int64_t)dd * tiles + blockIdx.x];
+        g_start[dd] = offs[(int64_t)dd * tiles + tile];
     }
     uint32_t key[kSlots];
     uint64_t val[kSlots];
