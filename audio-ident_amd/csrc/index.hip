@@ -5,8 +5,8 @@
 // `query` + offset voting (:185-202), whose per-track best bin becomes
 // OlafMatch.match_count (:44-50). SURVEY.md 8a rows a4, a5.
 //
-// Index (HBM): postings grouped by key26(hash) = k1 << 16 | k2 << 6 | dt (the 26
-// bits FPSPEC 6 can set), as a direct-address CSR:
+// Index (HBM): postings grouped by key26(hash) = bucket_key(hash) (aidfp_layout.h: a bit
+// permutation of the 26 bits FPSPEC 6 can set, k1 | k2 | dt), as a direct-address CSR:
 //   offsets u32[2^26 + 1]  (256 MB, one counting-sort pass, no comparison sort)
 //   post    u64[n]         (track | t_ref << 32)
 // Build = K4a count (one atomic per posting) -> exclusive scan -> K4b scatter.
@@ -37,9 +37,7 @@ constexpr int kTrackCap = 1024;  // LDS per-track best entries per query
 constexpr int kProbeMax = 512;
 constexpr int kHotLdsBits = 17;  // K5b stages hot bitmap rows of up to 2^17 bits (16 KB) in LDS
 
-__device__ __forceinline__ uint32_t key26(uint32_t h) {
-    return ((h >> 22) << 16) | (((h >> 12) & 0x3FFu) << 6) | (h & 0x3Fu);
-}
+__device__ __forceinline__ uint32_t key26(uint32_t h) { return bucket_key(h); }  // aidfp_layout.h
 
 __device__ __forceinline__ uint32_t mix_td(uint32_t track, int32_t d) {
     uint32_t x = track * 0x9E3779B1u ^ ((uint32_t)d * 0x85EBCA77u);

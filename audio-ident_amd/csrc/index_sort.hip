@@ -2,9 +2,10 @@
 // rocPRIM's onesweep kept only as an A/B reference (aid_engine_force K4_BUILD).
 //
 // Replaces the LMDB put of `olaf_c store` (audio-ident-service/app/audio/fingerprint.py:117-125;
-// SURVEY.md 8a row a4). The index is a direct-address CSR over key26 = k1 << 16 | k2 << 6 | dt
-// (index.hip); the build sorts the postings by key27 = key26, or 2^26 for a removed track's posting
-// (it sorts past every live key and is dropped), stably, so a bucket keeps arrival order.
+// SURVEY.md 8a row a4). The index is a direct-address CSR over key26 = bucket_key(hash) (aidfp_layout.h, a bit
+// permutation of k1 | k2 | dt that spreads the busy low bits over the three digit passes); the build sorts the
+// postings by key27 = key26, or 2^26 for a removed track's posting (it sorts past every live key and is dropped),
+// stably, so a bucket keeps arrival order.
 //
 // Hand-written sort (3 passes of 9-bit digits over bits 0..26, 512 digits per pass):
 //   count    per tile of kTile = 4096 postings, the digit histogram (LDS atomics) -> counts[digit][tile];
@@ -14,13 +15,16 @@
 //            running digit counters by LDS atomics issued back to back, cross-wave offsets), stages the tile
 //            in LDS in sorted order (48 KB: two workgroups per CU overlap one's loads with the other's
 //            ranking) and writes it out in runs of consecutive positions per digit.
-// Pass 1 reads the SoA postings (hash, track, t) itself (key generation fused in; the tombstones only when a
-// track is removed); pass 3 writes the values straight into the CSR's post array.
-// CSR offsets straight from the sorted keys: at the last posting i of each key's run, E[key + 1] = i + 1;
-// an inclusive max-scan of E over the 2^26 + 1 keys is offsets[] (an absent key inherits the end of the
-// largest key below it). No bucket-length atomics, no separate count of non-empty buckets.
-// Bytes per posting: 8 (count 1) + 24 (scatter 1) + 2 x (4 + 24) + 4 (run ends) = 92, against ~125 for the
-// rocPRIM build.
+// Pass 1 reads the SoA postings (hash, track, t) itself (key generation fused in; the tombstones and the track
+// column for the count only when a track is removed); pass 3 writes the values straight into the CSR's post array
+// and, instead of a sorted key array, the CSR's run ends: at the last posting i of each key's run,
+// E[key + 1] = i + 1 (a key's postings in one tile's digit run are contiguous and in key order; a run that may
+// continue in the next tile raises E by atomicMax). An inclusive max-scan of E over the 2^26 + 1 keys is
+// offsets[] (an absent key inherits the end of the largest key below it); it also counts the live keys (nonzero
+// E). No bucket-length atomics, no key array after the last pass.
+// Tiles are dealt XCD-contiguously (xcd_tile): adjacent tiles' partial lines complete in one L2.
+// Bytes per posting: 4 (count 1) + 24 (scatter 1) + 2 x 4 (counts 2, 3) + 24 (scatter 2) + 20 (scatter 3) = 80,
+// plus ~4 per distinct key (E) and the 2 KB of counts per tile per pass.
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "aidfp_device.h"
@@ -38,14 +42,11 @@ constexpr int kTile = kSortThreads * kSlots;    // 4096 postings per tile
 constexpr int kDigitsPerThread = kDigits / kSortThreads;
 static_assert(kDigitBits * kSortPasses == kSortKeyBits, "passes cover the key");
 
-__device__ __forceinline__ uint32_t sort_key26(uint32_t h) {
-    return ((h >> 22) << 16) | (((h >> 12) & 0x3FFu) << 6) | (h & 0x3Fu);  // = index.hip key26
-}
 
 // tomb == nullptr: no track is removed (the engine passes none then, saving a dependent load per posting)
 __device__ __forceinline__ uint32_t make_key(uint32_t h, uint32_t tr, const uint8_t *__restrict__ tomb,
                                              uint32_t n_tracks) {
-    return (tomb && tr < n_tracks && tomb[tr]) ? (1u << 26) : sort_key26(h);
+    return (tomb && tr < n_tracks && tomb[tr]) ? (1u << 26) : bucket_key(h);
 }
 
 // lanes of the wave holding the same 9-bit digit (among the lanes in `valid`)
@@ -92,7 +93,11 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
     for (int s = 0; s < kSlots; ++s) {  // all loads first
         const int64_t i = base + s * kSortThreads + tid;
         d[s] = 0xFFFFFFFFu;
-        if (i < n) d[s] = ((FIRST ? make_key(keys[i], ptrack[i], tomb, n_tracks) : keys[i]) >> shift) & (kDigits - 1);
+        if (i < n) {
+            // the track column only when a track is removed (tomb != nullptr: uniform)
+            const uint32_t k = !FIRST ? keys[i] : tomb ? make_key(keys[i], ptrack[i], tomb, n_tracks) : bucket_key(keys[i]);
+            d[s] = (k >> shift) & (kDigits - 1);
+        }
     }
 #pragma unroll
     for (int s = 0; s < kSlots; ++s)
@@ -114,7 +119,8 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
                                                                 int64_t n, int shift,
                                                                 const uint32_t *__restrict__ offs, int64_t tiles,
                                                                 uint32_t *__restrict__ keys_out,
-                                                                uint64_t *__restrict__ vals_out) {
+                                                                uint64_t *__restrict__ vals_out,
+                                                                uint32_t *__restrict__ E) {
     __shared__ uint32_t s_key[kTile];
     __shared__ uint64_t s_val[kTile];
     __shared__ uint32_t cnt[kSortWaves][kDigits];  // running per-wave counters, then cross-wave offsets
@@ -227,9 +233,20 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
         const uint32_t d = (k >> shift) & (kDigits - 1);
         const int64_t dst = (int64_t)g_start[d] + (i - (int)t_start[d]);
         if (dst >= n) continue;  // cannot happen for consistent counts; never write out of bounds
-        keys_out[dst] = k;
-        if (LAST) __builtin_nontemporal_store(s_val[i], &vals_out[dst]);
-        else vals_out[dst] = s_val[i];
+        if (LAST) {
+            // the run ends of the CSR, from the sorted tile itself (no key array is written): inside a digit run
+            // the tile's items are in full key order (stable passes), so a key change there is the key's last
+            // posting; the last item of a digit run may continue in a later tile, so it only raises E[k + 1]
+            // (every end is an atomicMax, so the true end -- the largest -- wins whatever the order)
+            if (k < (1u << 26)) {
+                const bool run_end = i + 1 == m || ((s_key[i + 1] >> shift) & (kDigits - 1)) != d;
+                if (run_end || s_key[i + 1] != k) atomicMax(&E[k + 1], (uint32_t)(dst + 1));
+            }
+            __builtin_nontemporal_store(s_val[i], &vals_out[dst]);
+        } else {
+            keys_out[dst] = k;
+            vals_out[dst] = s_val[i];
+        }
     }
 }
 
@@ -260,15 +277,25 @@ constexpr int kScanThreads = 1024, kScanItems = 8, kScanBlock = kScanThreads * k
 template <bool MAX>
 __device__ __forceinline__ uint32_t sop(uint32_t a, uint32_t b) { return MAX ? max(a, b) : a + b; }
 
+// nzc (MAX only, or nullptr): += the number of nonzero inputs (the live keys, for the offsets scan over E)
 template <bool MAX>
 __global__ __launch_bounds__(kScanThreads) void k_scan8(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                       int64_t n, uint32_t *__restrict__ bsum) {
+                                                       int64_t n, uint32_t *__restrict__ bsum,
+                                                       unsigned long long *__restrict__ nzc) {
     __shared__ uint32_t ws[kScanThreads / 64];
+    __shared__ uint32_t wnz[kScanThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t i0 = (int64_t)blockIdx.x * kScanBlock + (int64_t)tid * kScanItems;
     uint32_t v[kScanItems];
 #pragma unroll
     for (int j = 0; j < kScanItems; ++j) v[j] = i0 + j < n ? in[i0 + j] : 0u;
+    if (MAX && nzc) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < kScanItems; ++j) c += v[j] != 0u;
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if (lane == 0) wnz[w] = c;
+    }
     uint32_t incl[kScanItems];
     uint32_t acc = 0;
 #pragma unroll
@@ -291,6 +318,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan8(const uint32_t *__restri
         uint32_t t = 0;
         for (int i = 0; i < kScanThreads / 64; ++i) t = sop<MAX>(t, ws[i]);
         bsum[blockIdx.x] = t;
+        if (MAX && nzc) {
+            unsigned long long c = 0;
+            for (int i = 0; i < kScanThreads / 64; ++i) c += wnz[i];
+            atomicAdd(nzc, c);
+        }
     }
 }
 
@@ -316,11 +348,12 @@ static size_t scan8_tmp(int64_t n) {
 
 // MAX = false: exclusive sum; MAX = true: inclusive max
 template <bool MAX>
-static void scan8(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s) {
+static void scan8(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s,
+                  unsigned long long *nzc = nullptr) {
     if (n <= 0) return;
     const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
     uint32_t *bsum = tmp, *boff = tmp + nb;
-    hipLaunchKernelGGL(k_scan8<MAX>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, out, n, bsum);
+    hipLaunchKernelGGL(k_scan8<MAX>, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, out, n, bsum, nzc);
     if (nb > 1) {
         scan8<MAX>(bsum, boff, nb, tmp + 2 * nb + 8, s);
         if (MAX)  // boff = inclusive max of the block maxima: block b + 1 takes boff[b]
@@ -393,27 +426,27 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
         timed_launch(k_radix_count<true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
         scan8<false>(counts, offs, c, stmp, s);
         timed_launch(k_radix_scatter<true, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt, tomb,
-                     n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1);
+                     n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
         scan8<false>(counts, offs, c, stmp, s);
         timed_launch(k_radix_scatter<false, false>, g, b, 0, s, (const uint32_t *)keys1, (const uint64_t *)vals1,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
-                     kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0);
+                     kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0, (uint32_t *)nullptr);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys0, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, counts, tiles);
         scan8<false>(counts, offs, c, stmp, s);
         timed_launch(k_radix_scatter<false, true>, g, b, 0, s, (const uint32_t *)keys0, (const uint64_t *)vals0,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
-                     2 * kDigitBits, (const uint32_t *)offs, tiles, keys1, vals1);
-        sorted_keys = keys1;
+                     2 * kDigitBits, (const uint32_t *)offs, tiles, (uint32_t *)nullptr, vals1, E);
         *vals_out = vals1;
     }
-    if (n > 0) {
+    if (n > 0 && sorted_keys) {  // rocPRIM: run ends from its sorted keys
         const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_run_ends, dim3((unsigned)blocks), dim3(256), 0, s, sorted_keys, n, E, nz);
     }
-    scan8<true>(E, offsets, K, stmp, s);
+    // the hand-written sort wrote E in its last pass; its live keys are the nonzero E entries
+    scan8<true>(E, offsets, K, stmp, s, sorted_keys ? nullptr : nz);
     return hipGetLastError();
 }
 
