@@ -24,6 +24,9 @@ constexpr int kStftLdsPerWave = 1092;
 
 // K2: output frames per workgroup strip, sized per call (peak_strip_len) between these bounds
 constexpr int kPeakStripMin = 16;
+// ... and at most this long: K2 reads a strip's rows through one buffer descriptor with a 32-bit byte range
+// (peaks.hip), (kPeakStripMax + 2 x 7) rows x 4 KiB < 2^31
+constexpr int kPeakStripMax = 65536;
 
 // Smallest strip length L >= kPeakStripMin with sum_c ceil(F_c / L) <= slots (the resident K2
 // workgroups of the device): every strip then runs in the first (only) round. When the clips
@@ -37,6 +40,7 @@ inline int peak_strip_len(const int64_t *frames, int n, int64_t slots) {
         return k;
     };
     int64_t lo = kPeakStripMin, hi = fmax > lo ? fmax : lo;
+    if (hi > kPeakStripMax) hi = kPeakStripMax;  // longer clips take several strips (more than one round)
     if (count(lo) <= slots) return (int)lo;
     while (lo < hi) {  // count(L) is non-increasing in L
         const int64_t mid = (lo + hi) / 2;

@@ -128,6 +128,18 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
     const uint64_t *HW = hot + fb;
     const int myb = hot_bit(tid >> 2);
     auto hotword = [&](int r) -> uint64_t { return (r >= 0 && r < F) ? HW[r] : 0ull; };
+    // The loop's words come in through ONE vector load per step (lane l & 3 holds the word of row rb + (l & 3))
+    // and are read out with v_readlane: a scalar load shares lgkmcnt with the LDS, so the barrier after the
+    // staging (s_waitcnt lgkmcnt(0)) waited for the words just fetched, an L2/MALL round trip every 4 rows; the
+    // vector load is waited together with the row loads issued beside it (vmcnt, one step later)
+    auto hotwords = [&](int rb) -> uint64_t {
+        const int r = rb + (lane & 3);
+        return (r >= 0 && r < F) ? HW[r] : 0ull;
+    };
+    auto word_of = [](uint64_t v, int j) -> uint64_t {  // lane j's word, uniform (j compile-time)
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), j) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)v, j);
+    };
     // chunks 16w-1 .. 16w+16 hold the wave's bins and their +-15 neighbours
     uint64_t wmask = 0;
     for (int c = max(16 * wave - 1, 0); c <= min(16 * wave + 16, 63); ++c) wmask |= 1ull << hot_bit(c);
@@ -155,16 +167,23 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
             return;
         }
     }
+    // Row loads are range-checked buffer loads over the strip's rows (rlo .. rhi): a thread whose chunk is cold (or
+    // whose row lies outside the clip: hot word 0) passes an offset past the range and gets zeros without a branch
+    // (an exec-masked load with a zero-initialised phi made hipcc copy the loaded registers right after the load,
+    // behind an s_waitcnt vmcnt(0))
+    const int rlo = max(rbeg, 0), rhi = min(rbeg + iters, F);
+    const __amdgpu_buffer_rsrc_t rows_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(P + (int64_t)rlo * kBins), (short)0, (rhi - rlo) * kBins * 4, 0x00020000);
+    constexpr uint32_t kOOB = 0x80000000u;  // past any strip's byte count (< 2^31)
+    auto load_row = [&](int r, uint64_t hwr) -> float4 {
+        const uint32_t off = ((hwr >> myb) & 1ull) ? (uint32_t)(r - rlo) * (kBins * 4) + 16u * tid : kOOB;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rows_rsrc, off, 0, 0);
+        return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
+    };
     float4 pf[kRowsPerStep];  // rows of the next step, in flight
 #pragma unroll
-    for (int j = 0; j < kRowsPerStep; ++j) {
-        const int r = rbeg + j;
-        pf[j] = (j < iters && ((hotword(r) >> myb) & 1ull)) ? reinterpret_cast<const float4 *>(P + (int64_t)r * kBins)[tid]
-                                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    uint64_t hw[kRowsPerStep];  // hot words of the rows the next step fetches
-#pragma unroll
-    for (int j = 0; j < kRowsPerStep; ++j) hw[j] = hotword(rbeg + kRowsPerStep + j);
+    for (int j = 0; j < kRowsPerStep; ++j) pf[j] = load_row(rbeg + j, j < iters ? hotword(rbeg + j) : 0ull);
+    uint64_t hwv = hotwords(rbeg + kRowsPerStep);  // hot words of the rows the next step fetches (lane & 3)
     // hot words of the rows in flight (hsave) and of the rows being processed (hcur)
     uint64_t hsave[kRowsPerStep], hcur[kRowsPerStep];
 #pragma unroll
@@ -188,12 +207,10 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                     bms[j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
                     const int rn = rbeg + it + j + kRowsPerStep;
                     hcur[j] = hsave[j];
-                    hsave[j] = hw[j];
-                    pf[slot] = (it + j + kRowsPerStep < iters && ((hw[j] >> myb) & 1ull))
-                                   ? reinterpret_cast<const float4 *>(P + (int64_t)rn * kBins)[tid]
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-                    hw[j] = hotword(rn + kRowsPerStep);
+                    hsave[j] = word_of(hwv, j);
+                    pf[slot] = load_row(rn, it + j + kRowsPerStep < iters ? hsave[j] : 0ull);
                 }
+                hwv = hotwords(rbeg + it + 2 * kRowsPerStep);
                 __syncthreads();
             }
             const int r = rbeg + it;

@@ -346,6 +346,12 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                         hotw |= group16(hm >> 1) << (32 + 4 * i);
                         if (i > 0) hotw |= (hm & 1ull) << (31 + 4 * i);
                     }
+                    // Wait here for the next frame's ring loads (issued after the window multiply, a frame's work
+                    // ago: they have landed) and for the previous frame's stores. vmcnt counts loads and stores in
+                    // issue order, and this frame's stores are conditional: without this wait hipcc waits at the next
+                    // frame's window multiply with a count that only covers the unconditional stores, which also
+                    // waits for the L2 acknowledgement of the hot stores issued just before
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
                     {  // bin 512 pairs with itself: every lane computes it (same address, same value),
                        // so its store and the hot word's need no lane-0 branch
                         const float2 a = buf[2];  // Z[512] (E3 slot 2)
