@@ -56,11 +56,12 @@ static_assert(e1_region(15, 1) + 64 <= 2 * aid::kStftLdsPerWave, "E1 regions exc
 namespace aid {
 
 // 16-lane groups of a wave-wide mask -> 4 bits: bit g = some lane of lanes 16g .. 16g+15 is set (two
-// s_quadmask_b64: 64 lanes -> 16 quads -> 4 groups of 4 quads)
+// s_quadmask_b64: 64 lanes -> 16 quads -> 4 groups of 4 quads). s_quadmask writes SCC: without the clobber hipcc
+// may compute a branch condition into SCC before these and branch on it after them
 __device__ __forceinline__ uint64_t group16(uint64_t m) {
     uint64_t q, r;
-    asm("s_quadmask_b64 %0, %1" : "=s"(q) : "s"(m));
-    asm("s_quadmask_b64 %0, %1" : "=s"(r) : "s"(q));
+    asm("s_quadmask_b64 %0, %1" : "=s"(q) : "s"(m) : "scc");
+    asm("s_quadmask_b64 %0, %1" : "=s"(r) : "s"(q) : "scc");
     return r;
 }
 
