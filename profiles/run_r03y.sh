@@ -1,14 +1,17 @@
 #!/bin/bash
-# Round-3 consolidated run, part 2: config 4 (exact lane + robustness categories), config 5 (48 kHz index and a
-# 16 kHz index through K6), config 3 (catalog bench), the K4 probe under the tracer, the concurrency probe.
+# Round-3 consolidated run on the current build: full GPU suite, smoke, headline bench (all legs), a same-box A/B
+# against 2e8ff62 (build/prev: before the SCC clobber), rocprofv3 trace + FETCH/WRITE passes, SQ passes.
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r03y
 mkdir -p $O
-timeout -k 10 500 python bench_match.py > $O/match.json 2> $O/match.err
-timeout -k 10 300 python bench_stream.py > $O/stream48.json 2> $O/stream48.err
-timeout -k 10 300 python bench_stream.py --index-sr 16000 > $O/stream16.json 2> $O/stream16.err
-timeout -k 10 300 python bench_catalog.py > $O/catalog.json 2> $O/catalog.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/k4 -o run --output-format csv -- python3 probes/k4_probe.py > $O/k4.json 2> $O/k4.err
-timeout -k 10 300 python3 probes/concurrency_probe.py > $O/concurrency.json 2> $O/concurrency.err
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+for r in 1 2; do
+  AIDFP_LIB=audio-ident_amd/build/prev/libaidfp.so timeout -k 10 120 python3 bench.py --no-cpu --no-catalog --steps 50 > $O/ab_prev_$r.json 2>/dev/null
+  timeout -k 10 120 python3 bench.py --no-cpu --no-catalog --steps 50 > $O/ab_new_$r.json 2>/dev/null
+done
+bash profiles/run_rocprof.sh r03y > $O/prof.log 2>&1
+bash profiles/run_sq.sh r03y > $O/sq.log 2>&1
 echo done
