@@ -67,6 +67,31 @@ def test_match_rows_equal_oracle(catalog):
         assert abs(g[0, 2] * HOP - start) <= HOP
 
 
+def test_level_and_band_robustness(catalog):
+    """FPSPEC 5's peak threshold is absolute, so a query's recording level moves peaks across it. The index holds
+    unit-gain tracks; 5 s queries at 0 / -12 / -24 dB (20 dB SNR noise) and a 300-3400 Hz phone band must still
+    rank the true track first with its offset (the reference's exact-lane categories, scripts/eval_exact.py:46-54;
+    measured at scale in profiles/r03_config4_match.json). Runs before test_remove_and_save_load removes a track
+    from the shared catalog."""
+    from scipy.signal import butter, sosfilt
+
+    eng, tracks = catalog
+    rng = np.random.default_rng(11)
+    sos = butter(4, [300.0, 3400.0], btype="bandpass", fs=SR, output="sos")
+    qs, truth = [], []
+    for i in range(8):
+        tr = int(tracks[rng.integers(len(tracks))])
+        start = int(rng.integers(0, (TRACK_S - 5) * SR))
+        x = synth.synth(tr, start, 5 * SR, SR, snr_db=20.0, salt=300 + i).astype(np.float64)
+        for kind in ("0dB", "-12dB", "-24dB", "phone"):
+            y = sosfilt(sos, x) if kind == "phone" else x * 10.0 ** (float(kind[:-2]) / 20.0)
+            qs.append(y.astype(np.float32))
+            truth.append((tr, start, kind))
+    got = eng.query_pcm(qs)
+    for g, (tr, start, kind) in zip(got, truth):
+        assert len(g) > 0 and g[0, 1] == tr, f"{kind}: true track {tr} not first: {g[:3]}"
+        assert abs(g[0, 2] * HOP - start) <= HOP, kind
+
 def test_query_extracted_equals_host_query(catalog):
     eng, tracks = catalog
     rng = np.random.default_rng(7)
@@ -228,27 +253,3 @@ def test_sort_build_equals_atomic_build():
         assert np.array_equal(a, b), f"query {q}: rows differ between the builds"
         assert not np.isin(b[:, 1] if len(b) else [], [tracks[4], tracks[10]]).any()
 
-
-def test_level_and_band_robustness(catalog):
-    """FPSPEC 5's peak threshold is absolute, so a query's recording level moves peaks across it. The index holds
-    unit-gain tracks; 5 s queries at 0 / -12 / -24 dB (20 dB SNR noise) and a 300-3400 Hz phone band must still
-    rank the true track first with its offset (the reference's exact-lane categories, scripts/eval_exact.py:46-54;
-    measured at scale in profiles/r03_config4_match.json)."""
-    from scipy.signal import butter, sosfilt
-
-    eng, tracks = catalog
-    rng = np.random.default_rng(11)
-    sos = butter(4, [300.0, 3400.0], btype="bandpass", fs=SR, output="sos")
-    qs, truth = [], []
-    for i in range(8):
-        tr = int(tracks[rng.integers(len(tracks))])
-        start = int(rng.integers(0, (TRACK_S - 5) * SR))
-        x = synth.synth(tr, start, 5 * SR, SR, snr_db=20.0, salt=300 + i).astype(np.float64)
-        for kind in ("0dB", "-12dB", "-24dB", "phone"):
-            y = sosfilt(sos, x) if kind == "phone" else x * 10.0 ** (float(kind[:-2]) / 20.0)
-            qs.append(y.astype(np.float32))
-            truth.append((tr, start, kind))
-    got = eng.query_pcm(qs)
-    for g, (tr, start, kind) in zip(got, truth):
-        assert len(g) > 0 and g[0, 1] == tr, f"{kind}: true track {tr} not first: {g[:3]}"
-        assert abs(g[0, 2] * HOP - start) <= HOP, kind
