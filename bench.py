@@ -181,6 +181,7 @@ def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
     audio_mt = passes * sample.shape[0] * sample.shape[1] / SR
     audio_1 = one.shape[0] * one.shape[1] / SR
     np_leg = numpy_baseline(sample[:16], threads)
+    cat = catalog_cpu_estimate(O, ref, audio_mt / dt_mt, threads)
     return ref, {
         "value": round(audio_mt / dt_mt, 1),
         "unit": "audio-s/s",
@@ -194,7 +195,29 @@ def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
                   f"single-thread {audio_1 / dt_1:.1f} audio-s/s over {one.shape[0]} clips ({dt_1:.1f} s)",
         "single_thread": round(audio_1 / dt_1, 1),
         "numpy_scipy": np_leg,
+        "catalog": cat,
     }
+
+
+def catalog_cpu_estimate(O, ref: list, extract_rate: float, threads: int, tracks: int = 100000,
+                         track_s: float = 30.0, postings: int = 911675195) -> dict:
+    """Config 3 on the host (sub-sampled, extrapolated, labelled): the catalog's extraction at the
+    multi-thread oracle rate measured above, plus the index build as the oracle's sort (fp_index_sort, one thread)
+    of the batch's own postings, scaled n log n to the catalog's posting count (bench.py catalog leg)."""
+    p = np.concatenate([np.stack([(r & np.uint64(0xFFFFFFFF)).astype(np.uint32), np.full(len(r), c, np.uint32),
+                                  (r >> np.uint64(32)).astype(np.uint32)], axis=1) for c, r in enumerate(ref)])
+    p = np.ascontiguousarray(p)
+    t = time.perf_counter()
+    O.lib().fp_index_sort(O._ptr(p), len(p))
+    ts = time.perf_counter() - t
+    n = len(p)
+    sort_s = ts * (postings / n) * (np.log2(postings) / np.log2(max(n, 2)))
+    audio = tracks * track_s
+    extract_s = audio / extract_rate
+    return {"value": float(round(audio / (extract_s + sort_s), 1)), "unit": "audio-s/s", "extrapolated": True,
+            "sample": f"extraction at the {threads}-thread oracle rate above ({extract_s:.0f} s for {tracks} x "
+                      f"{track_s:.0f} s); index sort of the batch's {n} postings in {ts:.3f} s on one thread, scaled "
+                      f"n log n to {postings} postings ({sort_s:.0f} s)"}
 
 
 def _np_worker(args):

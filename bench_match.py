@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--min-match", type=int, default=0, help="engine min_match (0 = FPSPEC default)")
     ap.add_argument("--per-window", action="store_true", help="time the per-window path instead of aid_exact_lane")
     ap.add_argument("--category-queries", type=int, default=2000, help="positives per robustness category")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the host-oracle baseline")
+    ap.add_argument("--cpu-tracks", type=int, default=1000, help="index size of the host baseline (extrapolated)")
+    ap.add_argument("--cpu-clips", type=int, default=192, help="query clips of the host baseline")
     args = ap.parse_args()
 
     import torch
@@ -202,6 +205,84 @@ def run_batches(args, eng, truth, starts, n_pos, cat, pcm, clip_n, timed: bool):
             "median_offset_error_s": round(float(np.median(off_err)), 4) if off_err else None}, t_gpu
 
 
+def cpu_baseline(args, eng) -> dict:
+    """Config 4 on the host cores with the C oracle (sub-sampled, extrapolated, labelled): an
+    index of --cpu-tracks synthetic tracks (oracle fingerprints, sorted once, untimed like the GPU index build), then
+    --cpu-clips 5 s clips at the same SNR, each as the three 3.5 s sub-windows fingerprinted and queried
+    (oracle/fp_match.c fp_query) on a thread per core. A query's votes grow with the index (its buckets' lengths),
+    so the query part is scaled by index postings to --tracks; the extraction part is not."""
+    import ctypes
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "oracle"))
+    import oracle as O  # CPU baseline only
+    from aidfp import synth
+
+    sr, hop = args.sr, eng.hop
+    cores = len(os.sched_getaffinity(0))
+    try:  # cgroup CPU quota (the GPU box grants a share of a larger host)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            cores = max(1, min(cores, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    n = int(args.seconds * sr) & ~1
+    x = torch.empty(args.cpu_tracks * n, dtype=torch.float32, device="cuda")
+    tracks = np.arange(args.cpu_tracks, dtype=np.uint32)
+    eng.synth(x.data_ptr(), tracks, np.zeros(len(tracks), np.int64), n)
+    host = x.view(len(tracks), n).cpu().numpy()
+    del x
+    recs = O.fingerprint_batch(host, hop, threads=cores)
+    del host
+    post = np.concatenate([np.stack([(r & np.uint64(0xFFFFFFFF)).astype(np.uint32), np.full(len(r), t, np.uint32),
+                                     (r >> np.uint64(32)).astype(np.uint32)], axis=1) for t, r in zip(tracks, recs)])
+    post = np.ascontiguousarray(post)
+    O.lib().fp_index_sort(O._ptr(post), len(post))
+    rng = np.random.default_rng(7)
+    wlen = int(3.5 * sr) & ~1
+    noise_a = synth.noise_halfwidth(args.snr)
+    clips = []
+    for i in range(args.cpu_clips):
+        tr, st = int(rng.integers(0, args.cpu_tracks)), int(rng.integers(0, int(25 * sr)))
+        clips.append([synth.synth_int16(tr, st + int(a * sr), wlen, sr, noise_a, salt=77).astype(np.float32) / 32768.0
+                      for a in (0.0, 0.75, 1.5)])
+    rows = (O.Row * eng.max_results)()
+
+    def one(ws):
+        t_e = t_q = 0.0
+        hits = 0
+        for w in ws:
+            t = time.perf_counter()
+            r = O.fingerprint(np.ascontiguousarray(w, dtype=np.float32), hop)
+            t_e += time.perf_counter() - t
+            qh = np.ascontiguousarray((r & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+            qt = np.ascontiguousarray((r >> np.uint64(32)).astype(np.uint32))
+            out = (O.Row * eng.max_results)()
+            t = time.perf_counter()
+            hits += int(O.lib().fp_query(O._ptr(post), len(post), O._ptr(qh), O._ptr(qt), len(r), eng.min_match,
+                                         ctypes.addressof(out), eng.max_results))
+            t_q += time.perf_counter() - t
+        return t_e, t_q, hits
+
+    t = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        res = list(ex.map(one, clips))
+    wall = time.perf_counter() - t
+    t_e = sum(r[0] for r in res)
+    t_q = sum(r[1] for r in res)
+    scale = args.tracks / args.cpu_tracks
+    per_clip = (t_e + t_q * scale) / len(clips)  # core-seconds per clip at the full index
+    return {"value": round(cores / per_clip, 1), "unit": "clips/s", "cores": cores, "kind": "port",
+            "extrapolated": True, "measured_clips_per_s": round(len(clips) / wall, 1),
+            "sample": f"{len(clips)} clips x 3 sub-windows fingerprinted (oracle/fp_oracle.c) and queried "
+                      f"(oracle/fp_match.c) against a {args.cpu_tracks}-track index ({len(post)} postings) on {cores} "
+                      f"threads in {wall:.1f} s; core-seconds per clip {t_e / len(clips):.4f} extraction + "
+                      f"{t_q / len(clips):.4f} query, the query part scaled x{scale:.0f} to the {args.tracks}-track index"}
+
+
 def lane(args, eng, st, truth, starts, n_pos, n_neg, t_index) -> int:
     import torch
 
@@ -236,6 +317,7 @@ def lane(args, eng, st, truth, starts, n_pos, n_neg, t_index) -> int:
     sel = np.concatenate([np.arange(sub), n_pos + np.arange(sub_neg)])
     for name, cat in CATEGORIES.items():
         cats[name], _ = run_batches(args, eng, truth[sel], starts[sel], sub, cat, pcm, clip_n, False)
+    cpu = None if args.no_cpu else cpu_baseline(args, eng)
     print(json.dumps({
         "metric": "exact-lane clips/sec (5 s clips: 3 sub-window queries + consensus each), 1 GPU",
         "value": round(nq / t_gpu, 1), "unit": "clips/s", "engine_queries_per_s": round(3 * nq / t_gpu, 1),
@@ -245,7 +327,7 @@ def lane(args, eng, st, truth, starts, n_pos, n_neg, t_index) -> int:
         "median_offset_error_s": res["median_offset_error_s"],
         "engine_min_match": eng.min_match, "gpu_s": round(t_gpu, 3), "index_build_s": round(t_index, 3),
         "index_tracks": args.tracks, "index_postings": st.postings_total, "data": "synthetic",
-        "match_stats": ms, "kernels": kern, "roofline": roofline, "categories": cats,
+        "match_stats": ms, "kernels": kern, "roofline": roofline, "categories": cats, "cpu_baseline": cpu,
         "reference_targets": {"top1_clean": 0.98, "top1_mic": 0.75, "top1_browser": 0.70, "top5_mic": 0.85,
                               "offset_error_median_s": 0.5, "false_positive_rate": 0.02},
     }), flush=True)
