@@ -26,6 +26,11 @@
 // (commit c236449, the AID_K1_* switches).
 #include "aidfp_device.h"
 
+// The add-TID writes below set M0 inside their asm and name it as clobbered; clang warns that M0 is a reserved
+// register whose value it will not preserve across the asm. Nothing else in these kernels uses M0 (checked in the
+// disassembly: every M0 write is one of these asm blocks), so the warning (one per use, ~180 per build) is silenced.
+#pragma clang diagnostic ignored "-Winline-asm"
+
 // E1 layout. Each (k1, component) register of stage A goes lane-linear to its own 64-dword
 // region with ds_write_addtid_b32 (address = M0 + offset + 4 lane: no address VGPR, 2 LDS
 // cycles per instruction). Stage-A lane p holds n2 = e1_perm(p) = 4 (p & 15) + (p >> 4), so a
