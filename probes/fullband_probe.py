@@ -1,12 +1,10 @@
-"""K2 strip sizing on band-limited vs full-band audio: the bench batch (partials <= 8 kHz, -40 dBFS noise)
-and the same batch with uniform noise loud enough that most 64-bin blocks are hot at every frequency.
-Prints the per-launch K1/K2/K3 times for the engine's adaptive sizing (AIDFP_K2_SLOTS_X unset) or the
-fixed multiplier given in the environment. Diagnostic only.
+"""K2 strip sizing on band-limited vs full-band audio: the bench batch (partials <= 8 kHz) and the bench's full-band
+batch (partials <= 20 kHz), extracted with the engine's adaptive strip sizing and with fixed strips-per-slot
+multipliers (aid_engine_force K2_STRIPS_X100). Prints per-launch K1/K2/K3 times per setting. Diagnostic only.
 
-usage: [AIDFP_K2_SLOTS_X=1.5] python probes/fullband_probe.py
+usage: python probes/fullband_probe.py [x100 ...]     (0 = adaptive; default: 0 100 125 150 175 200)
 """
 import json
-import os
 import sys
 import time
 from pathlib import Path
@@ -32,8 +30,7 @@ def run(eng, pcm, offs, steps=40):
     dt = (time.perf_counter() - t) / steps
     prof = eng.profile_read(reset=True)
     eng.profile_enable(False)
-    return {"ms_per_step": round(dt * 1e3, 4),
-            **{k: round(ms / n, 4) for k, (ms, n) in prof.items() if n}}
+    return {"ms_per_step": round(dt * 1e3, 4), **{k: round(ms / n, 4) for k, (ms, n) in prof.items() if n}}
 
 
 def main():
@@ -41,17 +38,19 @@ def main():
 
     from aidfp.engine import Engine
 
+    settings = [int(a) for a in sys.argv[1:]] or [0, 100, 125, 150, 175, 200]
     eng = Engine(44100, device=0)
-    n = 441000
-    clips = 256
+    n, clips = 441000, 256
     pcm = torch.empty(clips * n, dtype=torch.float32, device="cuda")
     offs = np.arange(clips + 1, dtype=np.int64) * n
     tracks = np.arange(clips, dtype=np.uint32)
-    out = {"slots_x": os.environ.get("AIDFP_K2_SLOTS_X", "adaptive")}
-    eng.synth(pcm.data_ptr(), tracks, np.zeros(clips, np.int64), n)
-    out["band_limited"] = run(eng, pcm, offs)
-    eng.synth(pcm.data_ptr(), tracks, np.zeros(clips, np.int64), n, noise_a=6000)  # ~-15 dBFS uniform noise
-    out["full_band"] = run(eng, pcm, offs)
+    out = {}
+    for name, fmax in (("band_limited", 8000), ("full_band", 20000)):
+        eng.synth(pcm.data_ptr(), tracks + (0 if fmax == 8000 else 500000), np.zeros(clips, np.int64), n, fmax_hz=fmax)
+        for x in settings:
+            eng.force("k2_strips_x100", x)
+            out[f"{name}/{x or 'adaptive'}"] = run(eng, pcm, offs)
+    eng.force("k2_strips_x100", 0)
     print(json.dumps(out))
     eng.close()
 
