@@ -384,6 +384,12 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
         stats = eng.index_stats()
         audio = args.catalog_tracks * args.catalog_seconds
         gathered = 12 * sum(per_rank)  # bytes of (hash, track, t) every rank receives
+        exact = None
+        if args.exact_clips > 0:
+            try:
+                exact = exact_leg(eng, args, rank, world, dist, torch)
+            except Exception as exc:  # the catalog figure stands on its own
+                exact = {"error": f"{type(exc).__name__}: {exc}"}
         return {"value": round(audio / ingest, 1), "unit": "audio-s/s", "tracks": args.catalog_tracks,
                 "track_seconds": args.catalog_seconds, "ingest_s": round(ingest, 4),
                 "phase_s_max_over_ranks": {"extract": round(te, 4), "allgather": round(tx, 4), "build": round(tb, 4),
@@ -393,9 +399,42 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
                 "postings_held": int(stats["postings"]), "postings_live": int(stats["live"]),
                 "allgather_bytes_per_rank": gathered,
                 "allgather_gbs_per_rank": round(gathered / tx / 1e9, 1) if world > 1 and tx > 0 else None,
-                "union_equals_sum_of_shards": int(st.postings_total) == sum(per_rank)}
+                "union_equals_sum_of_shards": int(st.postings_total) == sum(per_rank),
+                "exact_lane": exact}
     finally:
         eng.close()
+
+
+def exact_leg(eng, args, rank, world, dist, torch) -> dict:
+    """BASELINE config 4 against the catalog this leg just built (every rank holds the whole union): per rank
+    args.exact_clips 5 s query clips (10 % from unseen tracks) at SNR 20 dB, mixed at half gain as the reference
+    corpus's noisy variant (bench_match.py "noise20"), through aid_exact_lane in 4096-clip calls (sub-window fan-out,
+    K1-K5 and the consensus in one call; reference app/search/exact.py:70-353). value = all ranks' clips / the
+    slowest rank's GPU time (weak scaling: queries are independent). Accuracy in the shape of
+    scripts/eval_exact.py:46-54 (top-1 target 0.98 on clean)."""
+    import types
+
+    from bench_match import CATEGORIES, run_batches
+
+    n = args.exact_clips
+    n_neg = n // 10
+    rng = np.random.default_rng(1000 + rank)
+    truth = np.concatenate([rng.integers(0, args.catalog_tracks, n - n_neg),
+                            np.arange(n_neg) + args.catalog_tracks + 10**6 + rank * n]).astype(np.uint32)
+    starts = np.concatenate([rng.integers(0, int((args.catalog_seconds - 5.0) * SR), n - n_neg),
+                             np.zeros(n_neg, np.int64)]).astype(np.int64)
+    clip_n = 5 * SR
+    batch = 4096
+    pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
+    a = types.SimpleNamespace(batch=batch, sr=SR)
+    cat = CATEGORIES["noise20"]
+    run_batches(a, eng, truth[:min(n, 256)], starts[:min(n, 256)], min(n, 256), cat, pcm, clip_n, False)  # warm-up
+    res, t_gpu = run_batches(a, eng, truth, starts, n - n_neg, cat, pcm, clip_n, True)
+    del pcm
+    t_max = _max_over_ranks(t_gpu, dist, torch)
+    return {"value": round(world * n / t_max, 1), "unit": "clips/s", "clips_per_rank": n, "gpu_s_max_over_ranks":
+            round(t_max, 4), "category": "noise20 (SNR 20 dB, gain 0.5)", "rank0": res,
+            "path": "aid_exact_lane, 4096 clips per call, 3 sub-windows each"}
 
 
 def main() -> int:
@@ -410,6 +449,8 @@ def main() -> int:
     ap.add_argument("--no-catalog", action="store_true", help="skip the config-3 catalog leg")
     ap.add_argument("--catalog-tracks", type=int, default=100000)
     ap.add_argument("--catalog-seconds", type=float, default=30.0)
+    ap.add_argument("--exact-clips", type=int, default=8192,
+                    help="config-4 query clips per rank against the catalog leg's index (0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print one line per rank and exit without touching the GPU (tests)")
     args = ap.parse_args()
