@@ -265,9 +265,11 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                 const int fm = max(max(L[i], p), R[i]);
                 const int m2 = max(fm, fprev[i]);
                 fprev[i] = fm;
+                // `before` reads the previous M7 ahead of the ring update, so the new M7 can take its register (with
+                // the update first, both were live together and every hot row ended in 4 phi copies)
+                const int bf = max(max(i == 0 ? max(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
                 m2r[s][i] = m2;
                 const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
-                const int bf = max(max(i == 0 ? max(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
                 m7p[i] = m7;
                 // row r-7 (slot s+1) has now met all 7 later rows: p >= their row-max
                 pk[i] = pend[(s + 1) & 7][i] >= m7;
@@ -281,7 +283,8 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
             const int rd = r - kPeakDT;
             if (rd >= t0 && rd < t1) {
                 // lane i < 4 stores ballot word i: 8 v_writelane of the SGPR ballots
-                uint32_t lo = 0, hi = 0;
+                uint32_t lo, hi;  // no zero init (2 VALU per row): only lanes 0..3 are stored
+                asm volatile("" : "=v"(lo), "=v"(hi));
                 lo = write_lane<0>(lo, (uint32_t)b0);
                 hi = write_lane<0>(hi, (uint32_t)(b0 >> 32));
                 lo = write_lane<1>(lo, (uint32_t)b1);
