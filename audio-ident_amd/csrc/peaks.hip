@@ -274,9 +274,10 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                 // row r-7 (slot s+1) has now met all 7 later rows: p >= their row-max
                 pk[i] = pend[(s + 1) & 7][i] >= m7;
                 bal[i] = __ballot(pk[i]);
-                // candidate: p > before (strict) and p >= right window, i.e. p >= max(before + 1, right)
-                // (integer keys <= 0x7F800000: no overflow); keys >= 0, so -1 = none
-                pend[s][i] = (p >= max(bf + 1, R[i])) ? p : -1;
+                // candidate: p > before (strict) and p >= right window; keys >= 0, so -1 = none
+                // two compares into SGPR masks and one s_and (3 VALU + 1 SALU) instead of add, max and one compare
+                // (4 VALU): K2 -2.5 % bench data, -3.5 % full-band (profiles/r03ah_k2_cmp2_ab.txt)
+                pend[s][i] = (p > bf && p >= R[i]) ? p : -1;
             }
             }
             const uint64_t b0 = bal[0], b1 = bal[1], b2 = bal[2], b3 = bal[3];
