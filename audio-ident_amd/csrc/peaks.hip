@@ -116,8 +116,9 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
         for (int i = 0; i < 4; ++i) { m2r[s][i] = 0; pend[s][i] = -1; }
 #pragma unroll
     for (int i = 0; i < 4; ++i) { fprev[i] = 0; m7p[i] = 0; }
-    // bin 0 is never a peak: its `before` bound is +inf
-    const int kmin_pen = (tid == 0) ? kInf : 0;
+    // bin 0 is never a peak: a uniform lane mask applied in the candidate test (SALU) instead of a per-lane +inf
+    // `before` bound (one VALU per row): K2 -0.7 % same-box (profiles/r03ai_k2_b0mask_ab.txt)
+    const uint64_t b0ok = __ballot(tid != 0);
 
     // iteration it processes row r = t0 - 7 + it and decides row r - 7
     const int rbeg = t0 - kPeakDT;
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                 fprev[i] = fm;
                 // `before` reads the previous M7 ahead of the ring update, so the new M7 can take its register (with
                 // the update first, both were live together and every hot row ended in 4 phi copies)
-                const int bf = max(max(i == 0 ? max(L[0], kmin_pen) : L[i], thr_row), m7p[i]);
+                const int bf = max(max(L[i], thr_row), m7p[i]);
                 m2r[s][i] = m2;
                 const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
                 m7p[i] = m7;
@@ -277,7 +278,9 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                 // candidate: p > before (strict) and p >= right window; keys >= 0, so -1 = none
                 // two compares into SGPR masks and one s_and (3 VALU + 1 SALU) instead of add, max and one compare
                 // (4 VALU): K2 -2.5 % bench data, -3.5 % full-band (profiles/r03ah_k2_cmp2_ab.txt)
-                pend[s][i] = (p > bf && p >= R[i]) ? p : -1;
+                bool cand = p > bf && p >= R[i];
+                if (i == 0) cand = cand && ((b0ok >> lane) & 1ull);
+                pend[s][i] = cand ? p : -1;
             }
             }
             const uint64_t b0 = bal[0], b1 = bal[1], b2 = bal[2], b3 = bal[3];
