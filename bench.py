@@ -428,7 +428,8 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
     a = types.SimpleNamespace(batch=batch, sr=SR)
     cat = CATEGORIES["noise20"]
-    run_batches(a, eng, truth[:min(n, 256)], starts[:min(n, 256)], min(n, 256), cat, pcm, clip_n, False)  # warm-up
+    w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a 4096-clip call is sized here
+    run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
     res, t_gpu = run_batches(a, eng, truth, starts, n - n_neg, cat, pcm, clip_n, True)
     del pcm
     t_max = _max_over_ranks(t_gpu, dist, torch)
