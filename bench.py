@@ -20,7 +20,8 @@ Extra keys of the line (none of them is `value`):
     extraction kernel, from the newest committed profiles/;
   * fullband -- the same batch with partials up to 20 kHz (no cold upper blocks);
   * catalog -- BASELINE config 3: 100k x 30 s tracks sharded over the ranks, extract +
-    the RCCL all-gather of the postings (aid_index_allgather) + the index build;
+    the RCCL all-gather of the postings (aid_index_allgather) + the index build; its exact_lane
+    sub-key is BASELINE config 4 against that index (8192 noisy 5 s clips per rank, aid_exact_lane);
   * cpu_baseline -- the bit-exact C oracle on the host cores, and the NumPy/SciPy path, on
     rank 0 at N=1 over bounded samples of the same clips.
 """
