@@ -20,7 +20,8 @@ AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
 AID_FLAG_KEEP_POWER = 1
-AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD = 1, 2, 3, 4, 5
+(AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD,
+ AID_FORCE_EXCHANGE_FAIL) = 1, 2, 3, 4, 5, 6
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
 AID_K_COUNT = 12
 KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample",
@@ -113,6 +114,7 @@ SIGNATURES = [
     ("aid_index_allgather", ctypes.c_int, [P, P, I64, P]),
     ("aid_comm_size", ctypes.c_int, [P, P, P]),
     ("aid_index_shard_info", ctypes.c_int, [P, I64, P, P]),
+    ("aid_index_reserve", ctypes.c_int, [P, I64, I64, ctypes.c_uint32, P]),
     ("aid_index_pack", ctypes.c_int, [P, I64, P, I64, P]),
     ("aid_index_splice", ctypes.c_int, [P, I64, P, I32, I64, P, ctypes.c_uint32, P]),
     ("aid_index_save", ctypes.c_int, [P, ctypes.c_char_p]),

@@ -39,30 +39,92 @@ def shard(tracks, rank: int, world: int):
     return tracks[lo:hi]
 
 
+class ExchangeAborted(RuntimeError):
+    """Raised on every rank when some rank could not take part in a collective step (its own error is
+    raised on that rank); no rank's index changed."""
+
+
+def agree(ok: bool, group=None) -> tuple[bool, int]:
+    """Collective: every rank learns whether all ranks are ok. Returns (all_ok, first failing rank or -1).
+    One all-gather of one int per rank (RCCL on a device tensor under "nccl", else gloo on the host)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return ok, (-1 if ok else 0)
+    world = dist.get_world_size(group)
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    mine = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev)
+    allf = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allf, mine, group=group)
+    flags = allf.cpu().tolist()
+    bad = [r for r, f in enumerate(flags) if not f]
+    return not bad, (bad[0] if bad else -1)
+
+
+def agreed(fn, what: str, group=None):
+    """Run the rank-local step `fn()`, then agree on it across the ranks before any later collective: a
+    failure on one rank raises on EVERY rank (its own exception there, ExchangeAborted elsewhere) instead
+    of leaving the others blocked in the next collective."""
+    err = None
+    out = None
+    try:
+        out = fn()
+    except Exception as exc:  # noqa: BLE001 - re-raised below on this rank
+        err = exc
+    ok, bad = agree(err is None, group)
+    if err is not None:
+        raise err
+    if not ok:
+        raise ExchangeAborted(f"{what}: rank {bad} failed; aborted on every rank")
+    return out
+
+
 def exchange_postings(eng, first: int = 0, group=None) -> int:
     """Replace this rank's postings [first, n) by the union of every rank's, in rank order, through
-    torch.distributed collectives around aid_index_pack / aid_index_splice. Returns the postings held.
+    torch.distributed collectives around aid_index_reserve / aid_index_pack / aid_index_splice. Returns
+    the postings held.
 
-    Under "nccl" the planes are all-gathered as device tensors; under gloo as host copies. `eng` needs
-    index_shard_info / index_pack / index_splice and device buffers from `eng.alloc_planes` when it has
-    one (tests use a host stand-in), else torch.cuda tensors."""
+    Every rank runs the same collectives whatever happens locally: the (count, n_tracks) all-gather, then
+    one ok flag after the local preparation (exchange buffers, the grown index, the pack), and the payload
+    only if every rank is ready -- a rank-local failure raises on every rank with the indexes unchanged
+    (native twin: aid_index_allgather). Under "nccl" the planes are all-gathered as device tensors; under
+    gloo as host copies. `eng` needs index_shard_info / index_pack / index_splice (index_reserve when it
+    has one) and device buffers from `eng.alloc_planes` when it has one (tests use a host stand-in), else
+    torch.cuda tensors."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     on_dev = dist.get_backend(group) == "nccl"
-    n, nt = eng.index_shard_info(first)
+    err = None
+    try:
+        n, nt = eng.index_shard_info(first)
+    except Exception as exc:  # noqa: BLE001 - still takes part in the counts round (count -1)
+        err, n, nt = exc, -1, 0
     meta = torch.tensor([n, nt], dtype=torch.int64, device="cuda" if on_dev else "cpu")
     allm = torch.empty(2 * world, dtype=torch.int64, device=meta.device)
     dist.all_gather_into_tensor(allm, meta, group=group)
     m = allm.view(world, 2).cpu().numpy()
+    if err is not None:
+        raise err
+    if (m[:, 0] < 0).any():
+        raise ExchangeAborted(f"index exchange: rank {int(np.argmax(m[:, 0] < 0))} has an invalid shard")
     counts, stride, tracks = m[:, 0].copy(), int(m[:, 0].max()), int(m[:, 1].max())
     alloc = getattr(eng, "alloc_planes", None) or (lambda k: torch.empty(k, dtype=torch.int32, device="cuda"))
-    send = alloc(3 * stride)
-    if stride:
-        eng.index_pack(first, send.data_ptr(), stride)
-    if on_dev:
+
+    def prepare():
+        send = alloc(3 * stride)
         recv = alloc(3 * stride * world)
+        reserve = getattr(eng, "index_reserve", None)
+        if reserve is not None:
+            reserve(first, int(counts.sum()), tracks)
+        if stride:
+            eng.index_pack(first, send.data_ptr(), stride)
+        return send, recv
+
+    send, recv = agreed(prepare, "index exchange (prepare)", group)
+    if on_dev:
         if stride:
             dist.all_gather_into_tensor(recv, send, group=group)
         torch.cuda.synchronize()  # the engine's stream reads what torch's stream gathered
@@ -70,7 +132,6 @@ def exchange_postings(eng, first: int = 0, group=None) -> int:
         recv_h = torch.empty(3 * stride * world, dtype=torch.int32)
         if stride:
             dist.all_gather_into_tensor(recv_h, send.cpu(), group=group)
-        recv = alloc(3 * stride * world)
         recv.copy_(recv_h)
     return eng.index_splice(first, recv.data_ptr() if stride else 0, counts, stride, tracks)
 
@@ -95,7 +156,7 @@ def native_comm(eng, group=None) -> int:
     import torch.distributed as dist
 
     rank = dist.get_rank(group)
-    obj = [eng.comm_id() if rank == 0 else None]
+    obj = [agreed(lambda: eng.comm_id() if rank == 0 else None, "RCCL unique id", group)]
     dist.broadcast_object_list(obj, src=0, group=group)
     return eng.comm_create(obj[0], dist.get_world_size(group), rank)
 
@@ -116,24 +177,31 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     n = int(round(seconds * eng.sample_rate)) & ~1
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pcm = torch.empty(max(1, min(batch, len(mine))) * n, dtype=torch.float32, device="cuda")
     base = eng.index_stats()["postings"]
-    # one non-default stream for generation, extraction and the posting append: events recorded on
-    # the legacy default stream would serialise against the engine's (blocking) stream every batch
-    s = torch.cuda.Stream()
-    torch.cuda.synchronize()
     ev = []
-    for b0 in range(0, len(mine), batch):
-        tr = mine[b0 : b0 + batch]
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(s)
-        eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
-        b.record(s)
-        ev.append((a, b))
-        eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n, s.cuda_stream)
-        eng.index_add_extracted(tr)
-    del pcm
-    torch.cuda.synchronize()
+
+    def extract_shard():
+        pcm = torch.empty(max(1, min(batch, len(mine))) * n, dtype=torch.float32, device="cuda")
+        # one non-default stream for generation, extraction and the posting append: events recorded on
+        # the legacy default stream would serialise against the engine's (blocking) stream every batch
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        for b0 in range(0, len(mine), batch):
+            tr = mine[b0 : b0 + batch]
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
+            b.record(s)
+            ev.append((a, b))
+            eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n, s.cuda_stream)
+            eng.index_add_extracted(tr)
+        del pcm
+        torch.cuda.synchronize()
+
+    if distributed and world > 1:
+        agreed(extract_shard, "catalog ingest (extract)", group)  # a failed shard stops every rank here
+    else:
+        extract_shard()
     t1 = time.perf_counter()
     t_synth = sum(a.elapsed_time(b) for a, b in ev) * 1e-3
     n_local = eng.index_stats()["postings"] - base
@@ -142,7 +210,7 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
     nranks = 0
     if world > 1 and exchange == "native":
         ti = time.perf_counter()
-        comm = native_comm(eng, group)
+        comm = native_comm(eng, group)  # collective; aid_index_allgather agrees on every rank's readiness itself
         t1 = time.perf_counter()
         t_init = t1 - ti
         try:

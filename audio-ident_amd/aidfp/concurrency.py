@@ -83,13 +83,28 @@ class RWLock:
 _STOP = object()
 
 
-class QueryCoalescer:
-    """Gathers concurrent requests into batches for `run_batch(payloads) -> results` (same order)."""
+def _size(payload) -> int:
+    """Bytes of a request payload for the batch cap (0 for payloads without a length)."""
+    try:
+        return len(payload)
+    except TypeError:
+        return 0
 
-    def __init__(self, run_batch: Callable[[Sequence], Sequence], window_s: float = 0.0005, max_batch: int = 256):
+
+class QueryCoalescer:
+    """Gathers concurrent requests into batches for `run_batch(payloads) -> results` (same order).
+
+    A batch closes at `max_batch` requests or when the next request would take its payload bytes
+    (`len(payload)`) past `max_batch_bytes` (that request opens the next batch; a single request larger
+    than the cap runs alone), so many long uploads never land in one engine call."""
+
+    def __init__(self, run_batch: Callable[[Sequence], Sequence], window_s: float = 0.0005, max_batch: int = 256,
+                 max_batch_bytes: int = 64 << 20):
         self._run = run_batch
         self.window_s = float(window_s)
         self.max_batch = int(max_batch)
+        self.max_batch_bytes = int(max_batch_bytes)
+        self._held = None  # the request that did not fit the previous batch
         self._q: queue.SimpleQueue = queue.SimpleQueue()
         self._thread: threading.Thread | None = None
         self._start_lock = threading.Lock()
@@ -122,10 +137,11 @@ class QueryCoalescer:
 
     def _loop(self) -> None:
         while True:
-            first = self._q.get()
+            first, self._held = (self._held, None) if self._held is not None else (self._q.get(), None)
             if first is _STOP:
                 return
             batch = [first]
+            nbytes = _size(first[0])
             stop = False
             deadline = time.monotonic() + self.window_s
             while len(batch) < self.max_batch:
@@ -142,9 +158,16 @@ class QueryCoalescer:
                 if item is _STOP:
                     stop = True
                     break
+                if nbytes + _size(item[0]) > self.max_batch_bytes:
+                    self._held = item  # opens the next batch
+                    break
+                nbytes += _size(item[0])
                 batch.append(item)
             self._dispatch(batch)
             if stop:
+                if self._held is not None:
+                    self._dispatch([self._held])
+                    self._held = None
                 return
 
     def _dispatch(self, batch) -> None:

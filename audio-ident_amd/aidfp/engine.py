@@ -77,7 +77,8 @@ class Engine:
         self.close()
 
     FORCE = {"k5_path": L.AID_FORCE_K5_PATH, "k5_parts": L.AID_FORCE_K5_PARTS, "k5_batch": L.AID_FORCE_K5_BATCH,
-             "k2_strips_x100": L.AID_FORCE_K2_STRIPS_X100, "k4_build": L.AID_FORCE_K4_BUILD}
+             "k2_strips_x100": L.AID_FORCE_K2_STRIPS_X100, "k4_build": L.AID_FORCE_K4_BUILD,
+             "exchange_fail": L.AID_FORCE_EXCHANGE_FAIL}
 
     def force(self, what: str, value: int) -> None:
         """Test hook (aid_engine_force): pin one of the engine's own code paths, e.g. force("k5_path", 2)."""
@@ -283,6 +284,11 @@ class Engine:
         n, nt = ctypes.c_int64(), ctypes.c_uint32()
         check(self._lib.aid_index_shard_info(self._h, int(first), ctypes.byref(n), ctypes.byref(nt)))
         return int(n.value), int(nt.value)
+
+    def index_reserve(self, first: int, total: int, n_tracks: int, stream: int | None = None) -> None:
+        """Grow the posting planes / track tables for a splice of `total` postings at `first` (index unchanged)."""
+        check(self._lib.aid_index_reserve(self._h, int(first), int(total), int(n_tracks),
+                                          ctypes.c_void_p(stream) if stream else None))
 
     def index_pack(self, first: int, planes_ptr: int, stride: int, stream: int | None = None) -> None:
         """Copy this rank's shard [first, n) into device planes [3][stride] (hash, track, t; zero padded)."""

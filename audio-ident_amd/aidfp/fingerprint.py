@@ -106,12 +106,14 @@ class FingerprintService:
     write-ahead journal, so a store or delete writes O(track) bytes, not the whole index)."""
 
     def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20,
-                 coalesce_window_s: float = 0.0005, max_batch: int = 256):
+                 coalesce_window_s: float = 0.0005, max_batch: int = 256, max_batch_bytes: int = 64 << 20):
         self.db_dir = Path(db_dir) if db_dir is not None else db_path()
         self.device = device
         self._rw = RWLock()  # index writers exclusive, queries shared
         self._init_lock = threading.Lock()  # first-use engine creation + index load
-        self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch)
+        # a coalesced batch holds at most max_batch requests and max_batch_bytes of PCM (64 MiB = 17 min of
+        # 16 kHz audio): many long uploads cannot land in one extraction
+        self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch, max_batch_bytes)
         self._ckpt_retry_at = 0.0  # monotonic time before which a failed auto-checkpoint is not retried
         self._engine = None
         self._store = None
@@ -161,8 +163,10 @@ class FingerprintService:
             except BaseException:
                 eng.close()
                 raise
-            self._engine, self._store = eng, store
-            self._ids, self._names, self._next = ids, names, nxt
+            # the maps first, the engine last: _eng()'s lock-free fast path returns as soon as _engine is set,
+            # and a reader that got it must find the names of the loaded tracks
+            self._ids, self._names, self._next, self._store = ids, names, nxt, store
+            self._engine = eng
         return self._engine
 
     @staticmethod
@@ -260,17 +264,27 @@ class FingerprintService:
     def query(self, pcm: bytes) -> list[OlafMatch]:
         return self._coalescer(pcm)
 
-    def _query_batch(self, pcms: list[bytes]) -> list[list[OlafMatch]]:
-        """One engine call for every query the coalescer gathered (under the shared lock)."""
+    def _query_rows(self, eng, pcms: list[bytes]) -> list:
+        """Engine rows per request. If the batch's engine call fails (one request's vote table overflows, a
+        large batch runs out of device memory), the batch is bisected and retried, so only the request that
+        fails on its own gets [] -- like one failing `olaf_c query` process (fingerprint.py:197-200)."""
         from ._lib import EngineError
 
+        try:
+            return eng.query_pcm([self._pcm(p) for p in pcms])
+        except EngineError as exc:
+            if len(pcms) == 1:
+                logger.error("aidfp query failed: %s", exc)
+                return [np.zeros((0, 5), np.int64)]
+            logger.warning("aidfp query batch of %d failed (%s); retrying in halves", len(pcms), exc)
+        h = len(pcms) // 2
+        return self._query_rows(eng, pcms[:h]) + self._query_rows(eng, pcms[h:])
+
+    def _query_batch(self, pcms: list[bytes]) -> list[list[OlafMatch]]:
+        """One engine call for every query the coalescer gathered (under the shared lock)."""
         with self._rw.read():
             eng = self._eng()
-            try:
-                rows = eng.query_pcm([self._pcm(p) for p in pcms])
-            except EngineError as exc:
-                logger.error("aidfp query batch of %d failed: %s", len(pcms), exc)
-                return [[] for _ in pcms]
+            rows = self._query_rows(eng, pcms)
             sec = eng.hop / eng.sample_rate
             outs = []
             for r in rows:

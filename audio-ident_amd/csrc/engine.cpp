@@ -213,6 +213,7 @@ struct aid_engine {
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
     int k5_path = 0;       // aid_engine_force K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int k5_parts = 0;      // aid_engine_force K5_PARTS: K5a key partitions per query (0 = by vote count)
+    int inject_exchange_fail = 0;  // aid_engine_force EXCHANGE_FAIL: the next exchange's prepare step fails (tests)
     bool k5_spec_ok = true;  // the previous query batch's heaviest query fitted the LDS path (speculation gate)
     // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
     int64_t st_queries = 0, st_votes = 0, st_post_reads = 0, st_q_global = 0, st_q_lds = 0, st_records = 0;
@@ -503,6 +504,10 @@ int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
             if (value < 0 || value > 3) return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 radix, 2 atomic, 3 rocPRIM");
             e->k4_mode = value == 2 ? 0 : value == 3 ? 1 : 2;
             e->index_dirty = true;
+            return AID_OK;
+        case AID_FORCE_EXCHANGE_FAIL:
+            if (value != 0 && value != 1) return fail(AID_ERR_INVALID, "EXCHANGE_FAIL: 0 or 1");
+            e->inject_exchange_fail = value;
             return AID_OK;
         default:
             return fail(AID_ERR_INVALID, "aid_engine_force: unknown path id");
@@ -1104,18 +1109,40 @@ static int reserve_postings(aid_engine *e, int64_t extra, hipStream_t s) {
     return AID_OK;
 }
 
-// grow the track tables to max_track_plus1 ids; the new tombstone buffer is allocated before anything
-// changes, so a failed growth leaves the engine as it was
+// wait for the engine's own streams (not the whole device: torch streams, other engines and ranks on the
+// same GPU keep running) before a buffer that in-flight engine work may read is freed
+static void sync_engine_streams(aid_engine *e, hipStream_t s) {
+    if (e->last_stream && e->last_stream != s) (void)hipStreamSynchronize(e->last_stream);
+    if (e->own_stream && e->own_stream != s) (void)hipStreamSynchronize(e->own_stream);
+    (void)hipStreamSynchronize(s);
+}
+
+// capacity of the track tables for max_track_plus1 ids, without changing the index: the new tombstone
+// buffer is allocated (and filled) before the old one goes, so a failed growth leaves the engine as it was
+static int reserve_tracks(aid_engine *e, uint32_t max_track_plus1, hipStream_t s) {
+    const size_t want = std::max<size_t>(max_track_plus1, 1024);
+    if (want <= e->tomb.n) return AID_OK;
+    DevBuf<uint8_t> nb;
+    HIP_TRY(nb.reserve(std::max(want, 2 * e->tomb.n)));
+    if (e->tomb.p) sync_engine_streams(e, s);  // in-flight queries may still read the old tombstones
+    if (e->n_tracks) {
+        // synchronous: the engine's tombstones must be whole in the new buffer before it replaces the old one
+        hipError_t he = hipMemcpyAsync(nb.p, e->h_tomb.data(), e->n_tracks, hipMemcpyHostToDevice, s);
+        if (he == hipSuccess) he = hipStreamSynchronize(s);
+        if (he != hipSuccess) {
+            nb.release();
+            return fail(AID_ERR_DEVICE, std::string("reserve_tracks: ") + hipGetErrorString(he));
+        }
+    }
+    std::swap(e->tomb, nb);
+    nb.release();
+    return AID_OK;
+}
+
+// grow the track tables to max_track_plus1 ids (reserve first: nothing changes if that fails)
 static int ensure_tracks(aid_engine *e, uint32_t max_track_plus1, hipStream_t s) {
     if (max_track_plus1 <= e->n_tracks) return AID_OK;
-    const size_t want = std::max<size_t>(max_track_plus1, 1024);
-    if (want > e->tomb.n) {
-        DevBuf<uint8_t> nb;
-        HIP_TRY(nb.reserve(std::max(want, 2 * e->tomb.n)));
-        if (e->tomb.p) (void)hipDeviceSynchronize();  // in-flight queries may still read the old tombstones
-        std::swap(e->tomb, nb);
-        nb.release();
-    }
+    if (int rc = reserve_tracks(e, max_track_plus1, s)) return rc;
     e->h_tomb.resize(max_track_plus1, 0);
     e->n_tracks = max_track_plus1;
     HIP_TRY(hipMemcpyAsync(e->tomb.p, e->h_tomb.data(), e->n_tracks, hipMemcpyHostToDevice, s));
@@ -1400,6 +1427,10 @@ int aid_comm_create(aid_engine *e, const uint8_t id[AID_COMM_ID_BYTES], int32_t 
     if (!e || !id || !out || world <= 0 || rank < 0 || rank >= world) return fail(AID_ERR_INVALID, "aid_comm_create: bad argument");
     *out = nullptr;
     HIP_TRY(hipSetDevice(e->device));
+    {
+        std::lock_guard<std::mutex> lk(e->mu);
+        HIP_TRY(e->g_meta.reserve(2 * (size_t)world + 2));  // the exchange's (count, n_tracks) and ok rounds
+    }
     ncclUniqueId u;
     std::memcpy(u.internal, id, AID_COMM_ID_BYTES);
     ncclComm_t c = nullptr;
@@ -1442,6 +1473,10 @@ static int shard_info_locked(aid_engine *e, int64_t first, int64_t *count, uint3
 }
 
 static int pack_locked(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, hipStream_t s) {
+    if (e->inject_exchange_fail) {  // test hook: this rank's prepare step fails as a device OOM would
+        e->inject_exchange_fail = 0;
+        return fail(AID_ERR_NOMEM, "index exchange: injected failure of this rank's pack (aid_engine_force)");
+    }
     const int64_t n = e->n_post - first;
     if (n > stride) return fail(AID_ERR_INVALID, "aid_index_pack: stride below the shard's count");
     const uint32_t *src[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
@@ -1451,6 +1486,20 @@ static int pack_locked(aid_engine *e, int64_t first, uint32_t *planes, int64_t s
         for (int q = 0; q < 3; ++q)
             HIP_TRY(hipMemsetAsync(planes + q * stride + n, 0, (stride - n) * sizeof(uint32_t), s));
     return AID_OK;
+}
+
+// everything a splice of `tot` postings at `first` (and n_tracks ids) can fail on, done before the exchange:
+// the posting planes and the tombstone buffer grow keeping every stored posting (n_post, not first) and
+// every tombstone; the index itself (n_post, n_tracks, the CSR) does not change
+static int splice_reserve_locked(aid_engine *e, int64_t first, int64_t tot, uint32_t n_tracks, hipStream_t s) {
+    if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "index exchange: first out of range");
+    if (tot < 0) return fail(AID_ERR_INVALID, "index exchange: negative posting count");
+    if (first + tot > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index exchange: more than 2^32 postings");
+    const size_t want = (size_t)std::max<int64_t>(first + tot, e->n_post);
+    if (int rc = grow_copy_u32(e->p_hash, e->n_post, want, s)) return rc;
+    if (int rc = grow_copy_u32(e->p_track, e->n_post, want, s)) return rc;
+    if (int rc = grow_copy_u32(e->p_t, e->n_post, want, s)) return rc;
+    return n_tracks > e->n_tracks ? reserve_tracks(e, n_tracks, s) : AID_OK;
 }
 
 // failure-atomic: everything that can fail (growth of the posting planes and track tables) happens before
@@ -1463,13 +1512,8 @@ static int splice_locked(aid_engine *e, int64_t first, const uint32_t *recv, int
         if (counts[r] < 0 || counts[r] > stride) return fail(AID_ERR_INVALID, "aid_index_splice: bad count");
         tot += counts[r];
     }
-    if (first + tot > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index exchange: more than 2^32 postings");
-    // grow keeping every stored posting (n_post, not first: nothing is dropped if this fails)
-    const size_t want = (size_t)std::max<int64_t>(first + tot, e->n_post);
-    if (int rc = grow_copy_u32(e->p_hash, e->n_post, want, s)) return rc;
-    if (int rc = grow_copy_u32(e->p_track, e->n_post, want, s)) return rc;
-    if (int rc = grow_copy_u32(e->p_t, e->n_post, want, s)) return rc;
-    if (int rc = ensure_tracks(e, n_tracks, s)) return rc;
+    if (int rc = splice_reserve_locked(e, first, tot, n_tracks, s)) return rc;
+    if (int rc = ensure_tracks(e, n_tracks, s)) return rc;  // capacity reserved: only the commit is left
     uint32_t *dst[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
     int64_t at = first;
     for (int r = 0; r < world; ++r) {
@@ -1489,6 +1533,15 @@ int aid_index_shard_info(aid_engine *e, int64_t first, int64_t *count, uint32_t 
     if (!e || !count || !n_tracks) return fail(AID_ERR_INVALID, "aid_index_shard_info: null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     return shard_info_locked(e, first, count, n_tracks);
+}
+
+int aid_index_reserve(aid_engine *e, int64_t first, int64_t total, uint32_t n_tracks, void *stream) {
+    if (!e) return fail(AID_ERR_INVALID, "aid_index_reserve: null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = pick_stream(e, stream);
+    if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    return splice_reserve_locked(e, first, total, n_tracks, s);
 }
 
 int aid_index_pack(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, void *stream) {
@@ -1514,6 +1567,19 @@ int aid_index_splice(aid_engine *e, int64_t first, const uint32_t *recv, int32_t
     return splice_locked(e, first, recv, world, stride, counts, n_tracks, s);
 }
 
+// one all-gather of an int64 pair per rank over the engine's meta buffer (reserved by aid_comm_create);
+// every rank calls it the same number of times, whatever its own state
+static int allgather_pair(aid_engine *e, aid_comm *c, int64_t a, int64_t b, std::vector<int64_t> &out, hipStream_t s) {
+    const int W = c->world;
+    const int64_t mine[2] = {a, b};
+    HIP_TRY(hipMemcpyAsync(e->g_meta.p, mine, sizeof(mine), hipMemcpyHostToDevice, s));
+    NCCL_TRY(ncclAllGather(e->g_meta.p, e->g_meta.p + 2, 2, ncclInt64, c->comm, s));
+    out.assign(2 * (size_t)W, 0);
+    HIP_TRY(hipMemcpyAsync(out.data(), e->g_meta.p + 2, out.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return AID_OK;
+}
+
 int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_total) {
     if (!e || !c || !c->comm) return fail(AID_ERR_INVALID, "aid_index_allgather: null argument");
     if (c->device != e->device) return fail(AID_ERR_INVALID, "aid_index_allgather: comm and engine on different devices");
@@ -1522,42 +1588,72 @@ int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_to
     hipStream_t s = e->own_stream;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     const int W = c->world;
-    // 1. (count, n_tracks) of every rank: sizes the padded exchange and the track tables. Every rank takes part
-    //    even when its own arguments are bad (a count of -1 fails all ranks alike instead of leaving them hanging)
+    if (e->g_meta.n < 2 * (size_t)W + 2) return fail(AID_ERR_STATE, "aid_index_allgather: comm not made for this engine");
+    // Every rank runs the same collectives whatever happens locally: (1) (count, n_tracks), (2) one ok flag
+    // per rank after every step that can fail locally, (3) the payload only when every rank is ready. A
+    // rank-local failure (bad arguments, OOM of the exchange buffers or the grown index, the pack) is
+    // therefore seen by all ranks before the payload all-gather, and every rank returns an error with its
+    // index unchanged instead of leaving its peers blocked in RCCL.
     int64_t n_local = -1;
     uint32_t nt = 0;
     const int bad = shard_info_locked(e, first, &n_local, &nt);
-    HIP_TRY(e->g_meta.reserve(2 * (size_t)W + 2));
-    const int64_t mine[2] = {bad ? -1 : n_local, (int64_t)nt};
-    HIP_TRY(hipMemcpyAsync(e->g_meta.p, mine, sizeof(mine), hipMemcpyHostToDevice, s));
-    NCCL_TRY(ncclAllGather(e->g_meta.p, e->g_meta.p + 2, 2, ncclInt64, c->comm, s));
-    std::vector<int64_t> meta(2 * (size_t)W);
-    HIP_TRY(hipMemcpyAsync(meta.data(), e->g_meta.p + 2, meta.size() * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    int64_t mx = 0;
+    std::vector<int64_t> meta;
+    if (int rc = allgather_pair(e, c, bad ? -1 : n_local, (int64_t)nt, meta, s)) return rc;
+    int64_t mx = 0, tot = 0;
     uint32_t tracks = 0;
     std::vector<int64_t> counts(W);
     for (int r = 0; r < W; ++r) {
         if (meta[2 * r] < 0) return bad ? bad : fail(AID_ERR_INVALID, "aid_index_allgather: another rank's shard is invalid");
         counts[r] = meta[2 * r];
         mx = std::max(mx, counts[r]);
+        tot += counts[r];
         tracks = std::max(tracks, (uint32_t)meta[2 * r + 1]);
     }
+    // 2. local preparation: the exchange buffers ([3][mx] own planes, [W][3][mx] received; scratch of this
+    //    call only: ~(W + 1) x 12 B per largest-shard posting), the grown index, the pack of the own shard
+    int rc = AID_OK;
     if (mx > 0) {
-        // 2. own shard as [3][mx] planes (the tail past n_local is padding), one all-gather
-        HIP_TRY(e->g_send.reserve(3 * (size_t)mx));
-        HIP_TRY(e->g_recv.reserve(3 * (size_t)mx * W));
-        if (int rc = pack_locked(e, first, e->g_send.p, mx, s)) return rc;
+        hipError_t he = e->g_send.reserve(3 * (size_t)mx);
+        if (he == hipSuccess) he = e->g_recv.reserve(3 * (size_t)mx * W);
+        if (he != hipSuccess)
+            rc = fail(he == hipErrorOutOfMemory ? AID_ERR_NOMEM : AID_ERR_DEVICE,
+                      std::string("index exchange buffers: ") + hipGetErrorString(he));
+        if (!rc) rc = splice_reserve_locked(e, first, tot, tracks, s);
+        if (!rc) rc = pack_locked(e, first, e->g_send.p, mx, s);
+        if (!rc) {
+            he = hipStreamSynchronize(s);
+            if (he != hipSuccess) rc = fail(AID_ERR_DEVICE, std::string("index exchange pack: ") + hipGetErrorString(he));
+        }
+    } else {
+        rc = splice_reserve_locked(e, first, 0, tracks, s);
+    }
+    const std::string local_err = rc ? g_err : std::string();
+    std::vector<int64_t> ok;
+    if (int rc2 = allgather_pair(e, c, rc ? 0 : 1, (int64_t)rc, ok, s)) {
+        e->g_send.release();
+        e->g_recv.release();
+        return rc2;
+    }
+    int failed = -1;
+    for (int r = 0; r < W && failed < 0; ++r)
+        if (!ok[2 * r]) failed = r;
+    if (failed >= 0) {
+        e->g_send.release();
+        e->g_recv.release();
+        if (rc) return fail(rc, local_err);
+        return fail(AID_ERR_STATE, "index exchange aborted: rank " + std::to_string(failed) +
+                                       " failed to prepare (error " + std::to_string(ok[2 * failed + 1]) +
+                                       "); this rank's index is unchanged");
+    }
+    if (mx > 0) {
+        // 3. one all-gather of the padded planes, then the union in rank order replaces this rank's shard
         NCCL_TRY(ncclAllGather(e->g_send.p, e->g_recv.p, 3 * (size_t)mx, ncclUint32, c->comm, s));
-        // 3. the union in rank order replaces this rank's shard
-        const int rc = splice_locked(e, first, e->g_recv.p, W, mx, counts.data(), tracks, s);
-        // the exchange buffers are (world + 1) x 12 B per largest-shard posting (12 GB at 8 x 12.5k tracks):
-        // scratch of this call only
+        rc = splice_locked(e, first, e->g_recv.p, W, mx, counts.data(), tracks, s);
         e->g_send.release();
         e->g_recv.release();
         if (rc) return rc;
-    } else if (int rc = ensure_tracks(e, tracks, s)) {
-        return rc;
+    } else if (int rc3 = ensure_tracks(e, tracks, s)) {
+        return rc3;
     }
     if (n_total) *n_total = e->n_post;
     return AID_OK;

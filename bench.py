@@ -29,6 +29,7 @@ Extra keys of the line (none of them is `value`):
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
@@ -312,9 +313,13 @@ def fullband_leg(eng, pcm, offs, stream, args, rank, torch, dist) -> dict:
     K1 stores and K2 loads the whole band (the headline data stops at 8 kHz, ~60 % cold blocks)."""
     tracks = np.arange(CLIPS, dtype=np.uint32) + np.uint32(rank * CLIPS + 500000)
     n = SR * CLIP_S
-    eng.synth(pcm.data_ptr(), tracks, np.zeros(CLIPS, np.int64), n, fmax_hz=20000)
-    run_steps(eng, pcm.data_ptr(), offs, stream, max(1, args.warmup), torch)
-    settle(eng, pcm.data_ptr(), offs, stream, args.settle, torch)
+
+    def warm():
+        eng.synth(pcm.data_ptr(), tracks, np.zeros(CLIPS, np.int64), n, fmax_hz=20000)
+        run_steps(eng, pcm.data_ptr(), offs, stream, max(1, args.warmup), torch)
+        settle(eng, pcm.data_ptr(), offs, stream, args.settle, torch)
+
+    _agreed(warm, "fullband (warm-up)", dist)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -325,7 +330,8 @@ def fullband_leg(eng, pcm, offs, stream, args, rank, torch, dist) -> dict:
     el = time.perf_counter() - t0
     el = _max_over_ranks(el, dist, torch)
     world = dist.get_world_size() if dist else 1
-    kern = breakdown(eng, pcm.data_ptr(), offs, stream, max(1, min(args.steps, 20)), torch)
+    kern = _agreed(lambda: breakdown(eng, pcm.data_ptr(), offs, stream, max(1, min(args.steps, 20)), torch),
+                   "fullband (breakdown)", dist)
     out = {"value": round(world * CLIPS * CLIP_S * args.steps / el, 1), "unit": "audio-s/s",
            "ms_per_step": round(el / args.steps * 1e3, 4), "hashes_per_step_per_gpu": int(eng.counts().sum()),
            "kernels": {k: round(v["ms_per_launch"], 5) for k, v in kern.items()},
@@ -338,6 +344,17 @@ def fullband_leg(eng, pcm, offs, stream, args, rank, torch, dist) -> dict:
         ref = O.fingerprint_batch(host, 512, threads=min(8, os.cpu_count() or 1))
         out["parity"] = {"clips": 4, "bit_exact": all(np.array_equal(eng.hashes(c), ref[c]) for c in range(4))}
     return out
+
+
+def _agreed(fn, what: str, dist):
+    """Run the rank-local step fn() and, at N > 1, agree on its success before any later collective
+    (aidfp.catalog.agreed): a failure on one rank raises on every rank instead of leaving the others
+    blocked in the next barrier / all-reduce."""
+    if not dist:
+        return fn()
+    from aidfp.catalog import agreed
+
+    return agreed(fn, what)
 
 
 def _max_over_ranks(x: float, dist, torch) -> float:
@@ -366,7 +383,10 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        st = ingest_synthetic(eng, tracks, args.catalog_seconds, batch=1024, exchange=exchange)
+        # ingest agrees on its own rank-local steps (extraction, the exchange's prepare round); the last
+        # agreement covers the index build
+        st = _agreed(lambda: ingest_synthetic(eng, tracks, args.catalog_seconds, batch=1024, exchange=exchange),
+                     "catalog ingest", dist)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -387,7 +407,7 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
         gathered = 12 * sum(per_rank)  # bytes of (hash, track, t) every rank receives
         exact = None
         if args.exact_clips > 0:
-            try:
+            try:  # exact_leg agrees on its rank-local part, so every rank takes this branch alike
                 exact = exact_leg(eng, args, rank, world, dist, torch)
             except Exception as exc:  # the catalog figure stands on its own
                 exact = {"error": f"{type(exc).__name__}: {exc}"}
@@ -408,34 +428,63 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
 
 def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     """BASELINE config 4 against the catalog this leg just built (every rank holds the whole union): per rank
-    args.exact_clips 5 s query clips (10 % from unseen tracks) at SNR 20 dB, mixed at half gain as the reference
-    corpus's noisy variant (bench_match.py "noise20"), through aid_exact_lane in 4096-clip calls (sub-window fan-out,
-    K1-K5 and the consensus in one call; reference app/search/exact.py:70-353). value = all ranks' clips / the
-    slowest rank's GPU time (weak scaling: queries are independent). Accuracy in the shape of
-    scripts/eval_exact.py:46-54 (top-1 target 0.98 on clean)."""
+    args.exact_clips 5 s query clips of catalog tracks plus 10 % more from unseen tracks, at SNR 20 dB mixed at
+    half gain as the reference corpus's noisy variant (bench_match.py "noise20"), through aid_exact_lane in
+    4096-clip calls (sub-window fan-out, K1-K5 and the consensus in one call; reference
+    app/search/exact.py:70-353). value = all ranks' clips / the slowest rank's GPU time (weak scaling: queries
+    are independent). Accuracy in the shape of scripts/eval_exact.py:46-54 (top-1 target 0.98 on clean). An
+    untimed second pass of the same clips with events on the K5 kernels gives the match roofline: 8 B per
+    posting K5 read + 8 B per query record / the K5 kernels' time (bench_match.py lane())."""
     import types
 
-    from bench_match import CATEGORIES, run_batches
+    from bench_match import CATEGORIES, HBM_PEAK_GBS as PEAK, K5_KERNELS, run_batches
 
-    n = args.exact_clips
-    n_neg = n // 10
+    n_pos = args.exact_clips
+    n_neg = n_pos // 10
+    n = n_pos + n_neg
     rng = np.random.default_rng(1000 + rank)
-    truth = np.concatenate([rng.integers(0, args.catalog_tracks, n - n_neg),
+    truth = np.concatenate([rng.integers(0, args.catalog_tracks, n_pos),
                             np.arange(n_neg) + args.catalog_tracks + 10**6 + rank * n]).astype(np.uint32)
-    starts = np.concatenate([rng.integers(0, int((args.catalog_seconds - 5.0) * SR), n - n_neg),
+    starts = np.concatenate([rng.integers(0, int((args.catalog_seconds - 5.0) * SR), n_pos),
                              np.zeros(n_neg, np.int64)]).astype(np.int64)
     clip_n = 5 * SR
     batch = 4096
-    pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
     a = types.SimpleNamespace(batch=batch, sr=SR)
     cat = CATEGORIES["noise20"]
-    w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a 4096-clip call is sized here
-    run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
-    res, t_gpu = run_batches(a, eng, truth, starts, n - n_neg, cat, pcm, clip_n, True)
-    del pcm
+
+    def local():
+        pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
+        w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a 4096-clip call is sized here
+        run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
+        res, t_gpu = run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, True)
+        # untimed: the same clips again with events on the K5 kernels and the posting counters
+        eng.match_stats(reset=True)
+        eng.profile_select(None)
+        eng.profile_enable(True)
+        eng.profile_read(reset=True)
+        run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, False)
+        prof = eng.profile_read(reset=True)
+        eng.profile_enable(False)
+        ms = eng.match_stats(reset=True)
+        del pcm
+        return res, t_gpu, prof, ms
+
+    res, t_gpu, prof, ms = _agreed(local, "exact lane", dist)
     t_max = _max_over_ranks(t_gpu, dist, torch)
-    return {"value": round(world * n / t_max, 1), "unit": "clips/s", "clips_per_rank": n, "gpu_s_max_over_ranks":
-            round(t_max, 4), "category": "noise20 (SNR 20 dB, gain 0.5)", "rank0": res,
+    k5_s = sum(prof[k][0] for k in K5_KERNELS if k in prof) * 1e-3
+    alg = 8 * ms["posting_reads"] + 8 * ms["records"]
+    roof = {"kernels": list(K5_KERNELS), "bound": "hbm", "unit": "GB/s", "peak": PEAK,
+            "algorithmic_bytes": alg, "k5_seconds": round(k5_s, 4),
+            "achieved": round(alg / k5_s / 1e9, 1) if k5_s else None,
+            "frac": round(alg / k5_s / 1e9 / PEAK, 4) if k5_s else None,
+            "per_kernel_ms": {k: round(prof[k][0], 3) for k in K5_KERNELS if k in prof and prof[k][1]},
+            "source": "rank 0, untimed second pass of the same clips with HIP events on the K5 kernels",
+            "note": "bytes = 8 B x postings K5 read (LDS path once per vote, global path once per K5a key partition "
+                    "+ once in K5b) + 8 B x query records; the vote histogram's atomics and the exact tables stay "
+                    "in LDS / the caches and are not counted"}
+    return {"value": round(world * n / t_max, 1), "unit": "clips/s", "clips_per_rank": n, "positives_per_rank": n_pos,
+            "negatives_per_rank": n_neg, "gpu_s_max_over_ranks": round(t_max, 4),
+            "category": "noise20 (SNR 20 dB, gain 0.5)", "rank0": res, "match_stats": ms, "roofline": roof,
             "path": "aid_exact_lane, 4096 clips per call, 3 sub-windows each"}
 
 
@@ -451,8 +500,9 @@ def main() -> int:
     ap.add_argument("--no-catalog", action="store_true", help="skip the config-3 catalog leg")
     ap.add_argument("--catalog-tracks", type=int, default=100000)
     ap.add_argument("--catalog-seconds", type=float, default=30.0)
-    ap.add_argument("--exact-clips", type=int, default=8192,
-                    help="config-4 query clips per rank against the catalog leg's index (0 = skip)")
+    ap.add_argument("--exact-clips", type=int, default=10000,
+                    help="config-4 positive query clips per rank against the catalog leg's index, plus 10 %% "
+                         "negatives from unseen tracks (BASELINE configs[3]: 10k; 0 = skip)")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print one line per rank and exit without touching the GPU (tests)")
     args = ap.parse_args()
@@ -491,12 +541,15 @@ def main() -> int:
         # AIDFP_BENCH_BACKEND=gloo: rehearsal of the N-rank path on fewer GPUs than ranks (ranks share
         # devices round-robin; RCCL refuses two ranks on one GPU). The driver's runs use RCCL, one GPU each.
         backend = os.environ.get("AIDFP_BENCH_BACKEND", "nccl")
+        # bounded collectives: every rank-local step is agreed on before the next collective (_agreed), and a
+        # hang that slips past that still ends within the timeout instead of holding the node
+        timeout = datetime.timedelta(seconds=float(os.environ.get("AIDFP_BENCH_PG_TIMEOUT", "300")))
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         else:
             torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
         world = dist.get_world_size()
         rank = dist.get_rank()
     else:
@@ -504,18 +557,21 @@ def main() -> int:
 
     from aidfp.engine import Engine
 
-    eng = Engine(SR, device=torch.cuda.current_device())
     n = SR * CLIP_S
-    pcm = torch.empty(CLIPS * n, dtype=torch.float32, device="cuda")
-    tracks = np.arange(CLIPS, dtype=np.uint32) + np.uint32(rank * CLIPS)
-    eng.synth(pcm.data_ptr(), tracks, np.zeros(CLIPS, np.int64), n)
     offs = np.arange(CLIPS + 1, dtype=np.int64) * n
     stream = torch.cuda.current_stream().cuda_stream
-    frames = CLIPS * eng.num_frames(n)
 
-    run_steps(eng, pcm.data_ptr(), offs, stream, max(0, args.warmup), torch)
-    settle_steps = settle(eng, pcm.data_ptr(), offs, stream, args.settle, torch)
-    hashes_per_step = int(eng.counts().sum())
+    def setup():
+        eng = Engine(SR, device=torch.cuda.current_device())
+        pcm = torch.empty(CLIPS * n, dtype=torch.float32, device="cuda")
+        tracks = np.arange(CLIPS, dtype=np.uint32) + np.uint32(rank * CLIPS)
+        eng.synth(pcm.data_ptr(), tracks, np.zeros(CLIPS, np.int64), n)
+        run_steps(eng, pcm.data_ptr(), offs, stream, max(0, args.warmup), torch)
+        settle_steps = settle(eng, pcm.data_ptr(), offs, stream, args.settle, torch)
+        return eng, pcm, settle_steps, int(eng.counts().sum())
+
+    eng, pcm, settle_steps, hashes_per_step = _agreed(setup, "headline (set-up)", dist)
+    frames = CLIPS * eng.num_frames(n)
 
     # events inside the timed region on K1 (stft_power, the dominant kernel) only: every timed launch
     # carries two dispatch-attached events, ~6 us of end-of-kernel work per launch on MI355X

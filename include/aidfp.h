@@ -99,6 +99,8 @@ int aid_engine_config(const aid_engine *e, aid_config *out);
 #define AID_FORCE_K5_BATCH 3       /* 0 default (2048), else global-path queries per launch */
 #define AID_FORCE_K2_STRIPS_X100 4 /* 0 adaptive, else 100 x K2 strips per resident workgroup slot */
 #define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B) */
+#define AID_FORCE_EXCHANGE_FAIL 6  /* 1: the next index exchange's pack (aid_index_pack, or the prepare step of
+                                      aid_index_allgather) fails with AID_ERR_NOMEM, once (rank-failure tests) */
 int aid_engine_force(aid_engine *e, int32_t what, int32_t value);
 
 /* Frames and worst-case record count of a clip of n samples (FPSPEC 1, 5). */
@@ -236,7 +238,11 @@ void aid_comm_destroy(aid_comm *c);
 /* Collective over all ranks of c: every rank's postings [first, n) (its shard) are all-gathered
  * (counts and track-id ranges first, then one padded SoA all-gather) and replace [first, n) by
  * the union in rank order; postings before `first` stay. The index is left dirty (finalize
- * next). *n_total = postings now held. Every rank must call it with the same comm. */
+ * next). *n_total = postings now held. Every rank must call it with the same comm.
+ * Failure agreement: after the counts, every rank reserves the exchange buffers and the grown
+ * index and packs its shard, then all ranks all-gather one ok flag; the payload all-gather runs
+ * only if every rank is ready. A rank-local failure therefore makes EVERY rank return an error
+ * (AID_ERR_STATE on the others) with its index unchanged, instead of leaving peers blocked in RCCL. */
 int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_total);
 /* The communicator's RCCL view: ranks (ncclCommCount) and this rank (ncclCommUserRank). */
 int aid_comm_size(const aid_comm *c, int32_t *world, int32_t *rank);
@@ -246,6 +252,10 @@ int aid_comm_size(const aid_comm *c, int32_t *world, int32_t *rank);
  * all-gather the planes into DEVICE recv [world][3][stride] -> aid_index_splice with the host counts
  * [world] and max n_tracks. Splice is failure-atomic: on error the index is unchanged. */
 int aid_index_shard_info(aid_engine *e, int64_t first, int64_t *count, uint32_t *n_tracks);
+/* Everything a splice of `total` postings at `first` with n_tracks ids can fail on (growth of the posting
+ * planes and the track tables), done ahead of the payload collective; the index itself does not change.
+ * A host-driven exchange calls it with aid_index_pack before it agrees on every rank's readiness. */
+int aid_index_reserve(aid_engine *e, int64_t first, int64_t total, uint32_t n_tracks, void *stream);
 int aid_index_pack(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, void *stream);
 int aid_index_splice(aid_engine *e, int64_t first, const uint32_t *recv, int32_t world, int64_t stride,
                      const int64_t *counts, uint32_t n_tracks, void *stream);

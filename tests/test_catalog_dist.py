@@ -22,10 +22,12 @@ from aidfp.catalog import exchange_postings, shard
 class HostEngine:
     """numpy model of the exchange's three C ABI steps on a host posting store [n, 3]."""
 
-    def __init__(self, post: np.ndarray, n_tracks: int):
+    def __init__(self, post: np.ndarray, n_tracks: int, fail_pack: bool = False):
         self.post = post.astype(np.uint32)
         self.n_tracks = n_tracks
         self._bufs = {}
+        self.fail_pack = fail_pack  # aid_engine_force(EXCHANGE_FAIL) stand-in: the pack fails as an OOM would
+        self.reserved = None
 
     def alloc_planes(self, k):
         t = torch.zeros(max(k, 1), dtype=torch.int32)
@@ -41,7 +43,12 @@ class HostEngine:
     def index_shard_info(self, first):
         return len(self.post) - first, self.n_tracks
 
+    def index_reserve(self, first, total, n_tracks):
+        self.reserved = (first, total, n_tracks)  # capacity only: the store itself does not change
+
     def index_pack(self, first, ptr, stride):
+        if self.fail_pack:
+            raise MemoryError("injected pack failure")
         v = self._view(ptr)
         n = len(self.post) - first
         assert n <= stride
@@ -93,6 +100,97 @@ def _worker(rank, world, port, q):
         q.put((rank, total, eng.post, eng.n_tracks))
     finally:
         dist.destroy_process_group()
+
+
+def _fail_worker(rank, world, port, q, bad_rank):
+    """A world whose rank `bad_rank` fails its pack: every rank must raise (no rank left blocked in the
+    payload all-gather) and every index must be unchanged."""
+    import time
+
+    from aidfp.catalog import ExchangeAborted
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = _blocks(world)[rank]
+        start = np.concatenate([KEEP, mine])
+        eng = HostEngine(start, n_tracks=100 * rank + len(mine), fail_pack=rank == bad_rank)
+        t = time.monotonic()
+        kind = "none"
+        try:
+            exchange_postings(eng, first=len(KEEP))
+        except ExchangeAborted:
+            kind = "aborted"
+        except MemoryError:
+            kind = "own"
+        # the group is still usable afterwards: the collectives stayed matched
+        after = exchange_postings(HostEngine(start, n_tracks=1), first=len(KEEP))
+        q.put((rank, kind, time.monotonic() - t, np.array_equal(eng.post, start), after))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad", [(2, 1), (3, 0)])
+def test_exchange_rank_failure_raises_everywhere(world, bad):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, q, bad)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    n_union = len(KEEP) + sum(len(b) for b in _blocks(world))
+    for r in range(world):
+        kind, dt, unchanged, after = res[r]
+        assert kind == ("own" if r == bad else "aborted")
+        assert dt < 60 and unchanged
+        assert after == n_union
+
+
+def _agreed_worker(rank, world, port, q):
+    from aidfp.catalog import ExchangeAborted, agreed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def step():
+            if rank == 1:
+                raise ValueError("rank-local failure")
+            return rank
+
+        try:
+            agreed(step, "leg")
+            kind = "none"
+        except ExchangeAborted:
+            kind = "aborted"
+        except ValueError:
+            kind = "own"
+        ok = agreed(lambda: rank, "next leg")  # still in step with each other
+        q.put((rank, kind, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_agreed_leg_failure_reaches_every_rank():
+    """bench.py's per-leg agreement: rank 1's exception is raised on rank 1 and ExchangeAborted on the others,
+    and the next collective still lines up."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agreed_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    try:
+        res = {r: (k, ok) for r, k, ok in (q.get(timeout=120) for _ in range(3))}
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert res == {0: ("aborted", 0), 1: ("own", 1), 2: ("aborted", 2)}
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -427,3 +427,65 @@ def test_failed_auto_checkpoint_keeps_operation(svc, tmp_path, monkeypatch):
     assert run(fp.olaf_index_track(_pcm_of(0.4), uuid.UUID(int=6))) is True  # backoff: no retry storm
     again = fp.FingerprintService(tmp_path / "db")
     assert again.query(_pcm_of(0.3))[0].reference_path == str(tid)
+
+
+def test_one_failing_request_does_not_blank_its_batch(svc, monkeypatch):
+    """A coalesced batch whose engine call fails (one request overflows its vote table, AID_ERR_STATE) is
+    bisected and retried: only the request that fails on its own gets [], every other request of the batch
+    still gets its rows (the reference's olaf_c processes failed one by one, fingerprint.py:197-200)."""
+    import time as _t
+
+    names = [uuid.UUID(int=2000 + i) for i in range(8)]
+    for i, n in enumerate(names):
+        assert run(fp.olaf_index_track(_pcm_of(0.1 * (i + 1)), n))
+    eng = svc._eng()
+    real = eng.query_pcm
+    calls = []
+    poison = np.float32(0.77)
+
+    def picky_query(clips):
+        calls.append(len(clips))
+        _t.sleep(0.005)  # later arrivals queue up: batches form
+        if any(len(c) and c[0] == poison for c in clips):
+            raise _lib.EngineError(-4, "query vote table overflow")
+        return real(clips)
+
+    monkeypatch.setattr(eng, "query_pcm", picky_query)
+
+    async def many():
+        pcms = [_pcm_of(0.1 * (i % 8 + 1)) for i in range(40)]
+        pcms[17] = _pcm_of(0.77)
+        return await asyncio.gather(*[fp.olaf_query(p) for p in pcms])
+
+    got = run(many())
+    assert got[17] == []
+    for i, rows in enumerate(got):
+        if i != 17:
+            assert rows and rows[0].reference_path == str(names[i % 8]), i
+    assert max(calls) > 1  # it was coalesced
+
+
+def test_coalescer_caps_batch_bytes():
+    """QueryCoalescer closes a batch before the next payload would pass max_batch_bytes; that payload opens
+    the next batch, and one payload above the cap runs alone."""
+    import threading
+
+    from aidfp.concurrency import QueryCoalescer
+
+    gate = threading.Event()
+    seen = []
+
+    def runner(ps):
+        gate.wait(5)
+        seen.append([len(p) for p in ps])
+        return [len(p) for p in ps]
+
+    c = QueryCoalescer(runner, window_s=0.05, max_batch=64, max_batch_bytes=100)
+    first = c.submit(b"x")  # the dispatcher takes it and blocks in runner until the rest are queued
+    futs = [c.submit(b"y" * n) for n in (40, 40, 40, 300, 10)]
+    gate.set()
+    assert first.result(5) == 1
+    assert [f.result(5) for f in futs] == [40, 40, 40, 300, 10]
+    c.close()
+    assert all(sum(b) <= 100 or len(b) == 1 for b in seen)
+    assert [300] in seen

@@ -65,6 +65,30 @@ def test_allgather_bad_arguments(gpu_engine):
         gpu_engine.comm_create(b"short", 1, 0)
 
 
+def test_allgather_injected_failure_world1(gpu_engine):
+    """aid_index_allgather's ok round: a failure of this rank's prepare step (injected through
+    aid_engine_force EXCHANGE_FAIL) returns an error after the agreement, the index is unchanged, and the
+    next exchange over the same communicator works (the collectives stayed matched)."""
+    from aidfp._lib import EngineError
+
+    eng = gpu_engine
+    eng.index_reset()
+    eng.extract_host([synth.synth(t, 0, SR * 6, SR, salt=5) for t in (1, 2, 3)])
+    eng.index_add_extracted(np.array([1, 2, 3], np.uint32))
+    before = eng.index_export()
+    comm = eng.comm_create(eng.comm_id(), 1, 0)
+    try:
+        eng.force("exchange_fail", 1)
+        with pytest.raises(EngineError, match="injected"):
+            eng.index_allgather(comm, 0)
+        assert np.array_equal(eng.index_export(), before)
+        assert eng.index_stats()["tracks"] == 4
+        assert eng.index_allgather(comm, 0) == len(before)  # the hook is one-shot
+        assert np.array_equal(eng.index_export(), before)
+    finally:
+        eng.comm_destroy(comm)
+
+
 def test_splice_failure_leaves_index(gpu_engine):
     """aid_index_splice validates before it touches the index: a bad count fails and nothing changes."""
     import torch
@@ -111,6 +135,78 @@ def _rank_worker(rank, world, port, q):
             q.put((rank, mine, total, union, eng.index_stats()["tracks"], recs, rows))
     finally:
         dist.destroy_process_group()
+
+
+def _fail_rank_worker(rank, world, port, q):
+    """World 2 on one GPU, rank 1's pack fails by injection: both ranks must raise, indexes unchanged."""
+    import os
+    import time
+
+    import torch.distributed as dist
+
+    from aidfp._lib import EngineError
+    from aidfp.catalog import ExchangeAborted, exchange_postings
+    from aidfp.engine import Engine
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with Engine(SR, device=0) as eng:
+            ids = [10 * rank + k for k in range(2 + rank)]
+            eng.extract_host([synth.synth(t, 0, SR * 6, SR, salt=5) for t in ids])
+            eng.index_add_extracted(np.array(ids, np.uint32))
+            mine = eng.index_export()
+            tracks = eng.index_stats()["tracks"]
+            if rank == 1:
+                eng.force("exchange_fail", 1)
+            t = time.monotonic()
+            kind = "none"
+            try:
+                exchange_postings(eng, 0)
+            except EngineError as exc:
+                kind = "own:" + str(exc)[:80]
+            except ExchangeAborted:
+                kind = "aborted"
+            dt = time.monotonic() - t
+            same = np.array_equal(eng.index_export(), mine) and eng.index_stats()["tracks"] == tracks
+            total = exchange_postings(eng, 0)  # the retry succeeds on both ranks
+            q.put((rank, kind, dt, same, total))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_rank_failure_on_one_gpu():
+    """The N-rank exchange's failure agreement with real engines: rank 1's pack fails (aid_engine_force
+    EXCHANGE_FAIL), rank 1 raises its own EngineError, rank 0 raises ExchangeAborted -- both within seconds,
+    neither blocked in the payload all-gather -- and both indexes are unchanged; a retry then succeeds."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fail_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            item = q.get(timeout=300)
+            res[item[0]] = item[1:]
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert res[0][0] == "aborted"
+    assert res[1][0].startswith("own:") and "injected" in res[1][0]
+    for r in (0, 1):
+        _, dt, same, total = res[r]
+        assert dt < 60 and same
+    assert res[0][3] == res[1][3] > 0
 
 
 def test_world2_exchange_on_one_gpu():
