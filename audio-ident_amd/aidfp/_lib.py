@@ -20,6 +20,7 @@ AID_ERR_STATE = -4
 AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
 AID_FLAG_KEEP_POWER = 1
+AID_SYNTH_STATIONARY = 1
 (AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD,
  AID_FORCE_EXCHANGE_FAIL) = 1, 2, 3, 4, 5, 6
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
@@ -98,6 +99,7 @@ SIGNATURES = [
     ("aid_spectrogram", ctypes.c_int, [P, P, I64, P, I64]),
     ("aid_synth", ctypes.c_int, [P, P, P, P, I32, I64, I32, ctypes.c_uint32, P]),
     ("aid_synth_band", ctypes.c_int, [P, P, P, P, I32, I64, I32, ctypes.c_uint32, I32, P]),
+    ("aid_synth_rate", ctypes.c_int, [P, P, P, P, I32, I64, I32, I32, ctypes.c_uint32, I32, I32, P]),
     ("aid_index_reset", ctypes.c_int, [P]),
     ("aid_index_add_extracted", ctypes.c_int, [P, P]),
     ("aid_index_add_postings", ctypes.c_int, [P, P, P, P, I64, I32]),

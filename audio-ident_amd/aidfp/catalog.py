@@ -162,26 +162,36 @@ def native_comm(eng, group=None) -> int:
 
 
 def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=None,
-                     exchange: str = "native") -> IngestStats:
+                     exchange: str = "native", source_sr: int | None = None, local: bool = False) -> IngestStats:
     """Fingerprint this rank's shard of synthetic tracks on its GPU, replicate the index.
 
-    `track_ids` is the full catalog (global ids); with torch.distributed initialised
-    each rank takes shard(track_ids, rank, world), otherwise the whole list."""
+    `track_ids` is the full catalog (global ids); with torch.distributed initialised (and `local` False)
+    each rank takes shard(track_ids, rank, world), otherwise the whole list. `source_sr`: the tracks are
+    synthesised at that rate and brought to the engine's rate by K6 per track, as ingest decodes every file
+    with ffmpeg `-ar 16000` (audio-ident-service/app/audio/decode.py:41-60); default: synthesised at the
+    engine's rate."""
     import torch
     import torch.distributed as dist
 
-    distributed = dist.is_available() and dist.is_initialized()
+    distributed = dist.is_available() and dist.is_initialized() and not local
     rank = dist.get_rank(group) if distributed else 0
     world = dist.get_world_size(group) if distributed else 1
     mine = np.asarray(shard(np.asarray(track_ids, dtype=np.uint32), rank, world), dtype=np.uint32)
-    n = int(round(seconds * eng.sample_rate)) & ~1
+    resample = source_sr is not None and int(source_sr) != eng.sample_rate
+    if resample:
+        n_src = int(round(seconds * source_sr)) & ~1
+        n = eng.resample_len(n_src, int(source_sr), eng.sample_rate) & ~1
+    else:
+        n = int(round(seconds * eng.sample_rate)) & ~1
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     base = eng.index_stats()["postings"]
     ev = []
 
     def extract_shard():
-        pcm = torch.empty(max(1, min(batch, len(mine))) * n, dtype=torch.float32, device="cuda")
+        nb = max(1, min(batch, len(mine)))
+        pcm = torch.empty(nb * n, dtype=torch.float32, device="cuda")
+        src = torch.empty(nb * n_src, dtype=torch.float32, device="cuda") if resample else None
         # one non-default stream for generation, extraction and the posting append: events recorded on
         # the legacy default stream would serialise against the engine's (blocking) stream every batch
         s = torch.cuda.Stream()
@@ -190,12 +200,19 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
             tr = mine[b0 : b0 + batch]
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
-            eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
+            if resample:  # each track decoded at its own rate, then K6 to the engine's (ffmpeg -ar per file)
+                eng.synth(src.data_ptr(), tr, np.zeros(len(tr), np.int64), n_src, stream=s.cuda_stream,
+                          sample_rate=int(source_sr))
+                for c in range(len(tr)):
+                    eng.resample_range(src.data_ptr() + 4 * c * n_src, 0, n_src, 1, int(source_sr), eng.sample_rate,
+                                       0, n, pcm.data_ptr() + 4 * c * n, stream=s.cuda_stream)
+            else:
+                eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
             b.record(s)
             ev.append((a, b))
             eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n, s.cuda_stream)
             eng.index_add_extracted(tr)
-        del pcm
+        del pcm, src
         torch.cuda.synchronize()
 
     if distributed and world > 1:

@@ -14,6 +14,11 @@ Signal of track ``tr`` at absolute sample ``i``:
   * a new "note" every ``sr // 4`` samples (250 ms), ``j = i // note_len``;
   * 8 partials ``p``: phase increment ``inc = inc_min + (R(tr,p,j) * inc_rng) >> 32``
     (100 Hz .. 8 kHz; ``fmax_hz`` widens the band, e.g. 20 kHz for the full-band workload), amplitude ``A = 983 + R(tr,p+8,j) % 2949`` (0.03 .. 0.12 FS),
+    times the note envelope (generator v2, default) ``A = (A * E) >> 16`` with
+    ``E = 65536 - (rel * 32768) // note_len``: every note decays linearly to half amplitude, as a struck or
+    plucked note, so a landmark's time locks to the note onset. v0 (``envelope=False``) kept constant
+    amplitudes: on a stationary note the peak frame is decided by noise, so an independent capture of
+    the same track (another rate, another noise floor) kept only ~2 % of the landmarks,
     phase ``ph = R(tr,p+16,j) + inc * (i - j*note_len)`` (mod 2^32),
     value ``(A * SIN[ph >> 20]) >> 15`` with ``SIN[k] = round(32767 sin(2 pi k / 4096))``;
   * base noise ``R(tr,24,i) % 1137 - 568`` (about -40 dBFS rms);
@@ -71,7 +76,7 @@ def noise_halfwidth(snr_db: float | None) -> int:
 
 
 def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt: int = 0,
-                fmax_hz: int = 8000) -> np.ndarray:
+                fmax_hz: int = 8000, envelope: bool = True) -> np.ndarray:
     """int32 array of int16-range samples of track ``track`` at absolute samples start..start+n."""
     if n <= 0:
         return np.zeros(0, dtype=np.int32)
@@ -80,12 +85,13 @@ def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt:
     i = np.arange(start, start + n, dtype=np.int64)
     j = i // note_len
     rel = (i - j * note_len).astype(np.uint64)
+    env = (65536 - (rel.astype(np.int64) * 32768) // note_len) if envelope else np.int64(65536)
     acc = np.zeros(n, dtype=np.int64)
     with np.errstate(over="ignore"):
         for p in range(N_PARTIALS):
             r = rnd(track, p, j).astype(np.uint64)
             inc = (np.uint64(inc_min) + ((r * np.uint64(inc_rng)) >> np.uint64(32))) & np.uint64(0xFFFFFFFF)
-            amp = 983 + (rnd(track, p + 8, j).astype(np.int64) % 2949)
+            amp = ((983 + (rnd(track, p + 8, j).astype(np.int64) % 2949)) * env) >> 16
             ph = (rnd(track, p + 16, j).astype(np.uint64) + inc * rel) & np.uint64(0xFFFFFFFF)
             acc += (amp * _SIN_TABLE[(ph >> np.uint64(20)).astype(np.int64)]) >> 15
         acc += rnd(track, 24, i).astype(np.int64) % 1137 - 568
@@ -95,9 +101,9 @@ def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt:
 
 
 def synth(track: int, start: int, n: int, sr: int, snr_db: float | None = None, salt: int = 0,
-          fmax_hz: int = 8000) -> np.ndarray:
+          fmax_hz: int = 8000, envelope: bool = True) -> np.ndarray:
     """float32 PCM in [-1, 1): int16 samples / 32768 (exact)."""
-    q = synth_int16(track, start, n, sr, noise_halfwidth(snr_db), salt, fmax_hz)
+    q = synth_int16(track, start, n, sr, noise_halfwidth(snr_db), salt, fmax_hz, envelope)
     return (q.astype(np.float32) / np.float32(32768.0)).astype(np.float32)
 
 

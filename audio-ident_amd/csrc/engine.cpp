@@ -32,7 +32,7 @@ void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, 
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
                       uint64_t *k2_cold_host, uint32_t k2_waves, bool one_chunk_each, hipStream_t s);
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
-                  int noise_a, uint32_t salt, int fmax_hz, const int16_t *sin_tab, hipStream_t s);
+                  int noise_a, uint32_t salt, int fmax_hz, bool envelope, const int16_t *sin_tab, hipStream_t s);
 int64_t resample_lds_floats(int up, int down, int J);
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
                      const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s);
@@ -801,11 +801,13 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     return AID_OK;
 }
 
-int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
-                   int64_t n, int32_t noise_a, uint32_t salt, int32_t fmax_hz, void *stream) {
-    if (!e || !dst || !tracks || !starts || n_clips < 0 || n < 0 || noise_a < 0)
+int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
+                   int64_t n, int32_t sample_rate, int32_t noise_a, uint32_t salt, int32_t fmax_hz, int32_t flags,
+                   void *stream) {
+    if (!e || !dst || !tracks || !starts || n_clips < 0 || n < 0 || noise_a < 0 || sample_rate <= 0)
         return fail(AID_ERR_INVALID, "aid_synth: bad argument");
-    if (fmax_hz <= 100 || 2 * (int64_t)fmax_hz > e->cfg.sample_rate)
+    if (flags & ~AID_SYNTH_STATIONARY) return fail(AID_ERR_INVALID, "aid_synth: unknown flags");
+    if (fmax_hz <= 100 || 2 * (int64_t)fmax_hz > sample_rate)
         return fail(AID_ERR_INVALID, "aid_synth: fmax_hz must be in (100, sample_rate / 2]");
     if (n_clips == 0 || n == 0) return AID_OK;
     std::lock_guard<std::mutex> lk(e->mu);
@@ -818,12 +820,18 @@ int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int6
     HIP_TRY(hipMemcpyAsync(e->synth_starts.p, starts, n_clips * sizeof(int64_t), hipMemcpyHostToDevice, s));
     {
         ProfScope ps(e, AID_K_SYNTH, s);
-        launch_synth(dst, e->synth_tracks.p, e->synth_starts.p, n_clips, n, e->cfg.sample_rate, noise_a, salt, fmax_hz,
-                     e->d_sin, s);
+        launch_synth(dst, e->synth_tracks.p, e->synth_starts.p, n_clips, n, sample_rate, noise_a, salt, fmax_hz,
+                     !(flags & AID_SYNTH_STATIONARY), e->d_sin, s);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));
     return AID_OK;
+}
+
+int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
+                   int64_t n, int32_t noise_a, uint32_t salt, int32_t fmax_hz, void *stream) {
+    if (!e) return fail(AID_ERR_INVALID, "aid_synth: null engine");
+    return aid_synth_rate(e, dst, tracks, starts, n_clips, n, e->cfg.sample_rate, noise_a, salt, fmax_hz, 0, stream);
 }
 
 int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips, int64_t n,

@@ -26,6 +26,7 @@ struct SynthParams {
     int32_t noise_a;    // query noise half-width (0 = none)
     uint32_t salt;
     uint32_t seed_mul;  // (SEED * 0x9E3779B9) mod 2^32
+    int32_t envelope;   // 1: each note decays linearly to half amplitude (generator v2); 0: stationary notes (v0)
 };
 
 __global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, const uint32_t *__restrict__ tracks,
@@ -41,12 +42,14 @@ __global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, const ui
     const uint32_t key = mix32(tr + sp.seed_mul);
     const int64_t j = i / sp.note_len;
     const uint32_t rel = (uint32_t)(i - j * sp.note_len);
+    // note envelope (Q16): 65536 at the onset down to ~32768 at the note's end
+    const int32_t env = sp.envelope ? 65536 - (int32_t)((rel * 32768u) / (uint32_t)sp.note_len) : 65536;
     int32_t acc = 0;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
         const uint32_t r = rnd(key, p, (uint32_t)j);
         const uint32_t inc = sp.inc_min + (uint32_t)(((uint64_t)r * sp.inc_rng) >> 32);
-        const int32_t amp = 983 + (int32_t)(rnd(key, p + 8, (uint32_t)j) % 2949u);
+        const int32_t amp = ((983 + (int32_t)(rnd(key, p + 8, (uint32_t)j) % 2949u)) * env) >> 16;
         const uint32_t ph = rnd(key, p + 16, (uint32_t)j) + inc * rel;
         acc += (amp * (int32_t)sin_tab[ph >> 20]) >> 15;
     }
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, const ui
 }
 
 void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int n_clips, int64_t n, int sr,
-                  int noise_a, uint32_t salt, int fmax_hz, const int16_t *sin_tab, hipStream_t s) {
+                  int noise_a, uint32_t salt, int fmax_hz, bool envelope, const int16_t *sin_tab, hipStream_t s) {
     if (n <= 0 || n_clips <= 0) return;
     SynthParams sp;
     sp.n = n;
@@ -70,6 +73,7 @@ void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int
     sp.noise_a = noise_a;
     sp.salt = salt;
     sp.seed_mul = (uint32_t)((42ull * 0x9E3779B9ull) & 0xFFFFFFFFull);
+    sp.envelope = envelope ? 1 : 0;
     const int64_t blocks = (int64_t)n_clips * ((n + 255) / 256);
     hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(256), 0, s, out, tracks, starts, n_clips, sp, sin_tab);
 }

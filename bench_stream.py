@@ -31,6 +31,9 @@ def main() -> int:
     ap.add_argument("--chunk-s", type=float, default=2.5)
     ap.add_argument("--index-sr", type=int, default=48000,
                     help="index rate; != 48000 resamples the stream on the GPU (16000 = the reference's Olaf rate)")
+    ap.add_argument("--source-sr", type=int, default=44100,
+                    help="rate the catalog tracks are synthesised at before K6 brings them to --index-sr, as ingest "
+                         "decodes each file with ffmpeg -ar (decode.py:41-60); 0 = synthesise at the index rate")
     args = ap.parse_args()
     SR = 48000
     ISR = args.index_sr
@@ -43,7 +46,7 @@ def main() -> int:
 
     torch.cuda.set_device(0)
     eng = Engine(ISR, device=0)
-    ingest_synthetic(eng, np.arange(args.tracks, dtype=np.uint32), 30.0)
+    ingest_synthetic(eng, np.arange(args.tracks, dtype=np.uint32), 30.0, source_sr=args.source_sr or None)
     rng = np.random.default_rng(42)
     seg = 30 * SR
     n_seg = int(args.minutes * 60 / 30)
@@ -77,7 +80,7 @@ def main() -> int:
     stream_s = len(stereo) / SR
     print(json.dumps({
         "metric": "48 kHz stereo stream, 5 s / 2.5 s windows: sustained audio-s/s, 1 GPU",
-        "index_sr": ISR, "front_end": "downmix" if ISR == SR else f"downmix + resample 48000 -> {ISR} (K6)",
+        "index_sr": ISR, "index_source_sr": args.source_sr or ISR, "front_end": "downmix" if ISR == SR else f"downmix + resample 48000 -> {ISR} (K6)",
         "value": round(stream_s / total, 1), "unit": "audio-s/s", "n_gpus": 1,
         "stream_s": stream_s, "windows": len(results), "chunk_s": args.chunk_s,
         "push_latency_ms": {p: round(1e3 * float(np.percentile(lat, q)), 3) for p, q in (("p50", 50), ("p95", 95), ("p99", 99))},

@@ -147,6 +147,14 @@ int aid_synth(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *
    bench's full-band workload, whose spectrum has no cold upper blocks. aid_synth = fmax_hz 8000. */
 int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
                    int64_t n, int32_t noise_a, uint32_t salt, int32_t fmax_hz, void *stream);
+/* Same audio at an explicit sample rate (the engine's own rate above): the same partials and notes sampled
+   at `sample_rate`, e.g. a 44.1 kHz catalog or a 48 kHz capture for an engine that indexes at 16 kHz.
+   flags: AID_SYNTH_STATIONARY = the v0 generator (constant amplitude within a note); default = v2 (every
+   note decays linearly to half amplitude, as a struck or plucked note: landmark times lock to the onsets). */
+#define AID_SYNTH_STATIONARY 1
+int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
+                   int64_t n, int32_t sample_rate, int32_t noise_a, uint32_t salt, int32_t fmax_hz, int32_t flags,
+                   void *stream);
 
 /* ---- index + match (FPSPEC 7) ----
  * Replaces `olaf_c store` + LMDB (fingerprint.py:117-125), `olaf_c del` (:239-246) and

@@ -24,7 +24,8 @@ CLIPS = [
 
 out = {}
 for i, c in enumerate(CLIPS):
-    x = synth.synth(c["track"], c["start"], c["n"], c["sr"], snr_db=c["snr"], salt=c["salt"])
+    x = synth.synth(c["track"], c["start"], c["n"], c["sr"], snr_db=c["snr"], salt=c["salt"],
+                    envelope=c.get("envelope", False))  # oracle_v0.* holds v0-generator inputs
     out[f"pcm_{i}"] = x
     out[f"rec_{i}"] = O.fingerprint(x, c["hop"])
     out[f"pow_{i}"] = O.stft_power(x, c["hop"])[:4]

@@ -108,6 +108,23 @@ def test_batch_256_full_config(gpu_engine):
         assert np.array_equal(gpu_engine.hashes(c), ref[c]), f"clip {c}"
 
 
+@pytest.mark.parametrize("sr,envelope,noise", [(44100, True, 0), (44100, False, 300), (48000, True, 120),
+                                               (16000, False, 0), (22050, True, 50)])
+def test_synth_generators_bit_identical(gpu_engine, sr, envelope, noise):
+    """aid_synth_rate (both generators, explicit rates, query noise) equals aidfp.synth bit for bit."""
+    import torch
+
+    n = sr * 2 + 5
+    tracks = np.array([3, 70001, 12], np.uint32)
+    starts = np.array([0, sr // 3, 7 * sr], np.int64)
+    pcm = torch.empty(len(tracks) * n, dtype=torch.float32, device="cuda")
+    gpu_engine.synth(pcm.data_ptr(), tracks, starts, n, noise_a=noise, salt=9, sample_rate=sr, envelope=envelope)
+    host = pcm.cpu().numpy().reshape(len(tracks), n)
+    for c in range(len(tracks)):
+        ref = synth.synth_int16(int(tracks[c]), int(starts[c]), n, sr, noise, 9, envelope=envelope)
+        assert np.array_equal(host[c], (ref.astype(np.float32) / np.float32(32768.0)).astype(np.float32)), c
+
+
 def test_logmag_tolerance(gpu_engine):
     """STFT magnitudes within 1e-4 rel (frame-normalised), log-mag within 60 dB of the peak."""
     x = _clip(3, 220500, snr=20)

@@ -102,16 +102,20 @@ def test_stream_resampled_buffer_equals_whole_stream():
 
 
 def test_48k_stereo_stream_against_16k_index():
-    """The reference's setting: 48 kHz capture, 16 kHz fingerprints (fingerprint.py:10).
+    """The reference's deployment shape: the catalog ingested from 44.1 kHz files decoded to 16 kHz
+    (ffmpeg -ar 16000, decode.py:41-60; here K6 per track), queried by 48 kHz stereo capture
+    (AudioRecorder.svelte:86-106) downmixed and resampled to 16 kHz (fingerprint.py:10).
 
     Parity: every window's rows equal those of the CPU route (oracle resampling of the whole
-    stream -> window slice -> oracle fingerprint -> query). Identification is a soft floor:
-    the 48 kHz synth resampled is not the 16 kHz synth (partials near the new Nyquist are
-    filtered), so fewer landmarks survive than in a same-rate stream."""
+    stream -> window slice -> oracle fingerprint -> query). Identification: top-1 >= 0.98 on windows
+    inside a segment (scripts/eval_exact.py:46-54's clean target). The capture shares nothing
+    sample-exact with the index (other rate, other noise), so this needs the v2 generator's note
+    envelopes: with stationary v0 notes the peak frame on a note's plateau is decided by noise and
+    top-1 was 0.66-0.74."""
     with Engine(16000) as eng:
         from aidfp.catalog import ingest_synthetic
 
-        ingest_synthetic(eng, np.arange(30, dtype=np.uint32), 30.0)  # synth at 16 kHz
+        ingest_synthetic(eng, np.arange(30, dtype=np.uint32), 30.0, source_sr=44100)
         order = [4, 21, 11]
         seg = 30 * 48000
         L = np.concatenate([synth.synth(t, 0, seg, 48000, snr_db=30.0, salt=1) for t in order])
@@ -131,4 +135,4 @@ def test_48k_stereo_stream_against_16k_index():
         assert len(inside) >= 25
         hits = [r.best_track == order[int(r.start_s // 30)] for r in inside]
         wrong = [(r.start_s, r.best_track, int(r.rows[0, 0]) if len(r.rows) else 0) for r, h in zip(inside, hits) if not h]
-        assert np.mean(hits) >= 0.7, (np.mean(hits), wrong)
+        assert np.mean(hits) >= 0.98, (np.mean(hits), wrong)
