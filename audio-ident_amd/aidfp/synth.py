@@ -11,16 +11,21 @@ variants at a target SNR in dB (``build_eval_corpus.py:154-198``, default 20 dB
 at ``:602-606``) and query offsets drawn uniformly (``:481-483``).
 
 Signal of track ``tr`` at absolute sample ``i``:
-  * a new "note" every ``sr // 4`` samples (250 ms), ``j = i // note_len``;
   * 8 partials ``p``: phase increment ``inc = inc_min + (R(tr,p,j) * inc_rng) >> 32``
-    (100 Hz .. 8 kHz; ``fmax_hz`` widens the band, e.g. 20 kHz for the full-band workload), amplitude ``A = 983 + R(tr,p+8,j) % 2949`` (0.03 .. 0.12 FS),
-    times the note envelope (generator v2, default) ``A = (A * E) >> 16`` with
-    ``E = 65536 - (rel * 32768) // note_len``: every note decays linearly to half amplitude, as a struck or
-    plucked note, so a landmark's time locks to the note onset. v0 (``envelope=False``) kept constant
-    amplitudes: on a stationary note the peak frame is decided by noise, so an independent capture of
-    the same track (another rate, another noise floor) kept only ~2 % of the landmarks,
-    phase ``ph = R(tr,p+16,j) + inc * (i - j*note_len)`` (mod 2^32),
-    value ``(A * SIN[ph >> 20]) >> 15`` with ``SIN[k] = round(32767 sin(2 pi k / 4096))``;
+    (100 Hz .. 8 kHz; ``fmax_hz`` widens the band, e.g. 20 kHz for the full-band workload), amplitude
+    ``A = 983 + R(tr,p+8,j) % 2949`` (0.03 .. 0.12 FS), phase ``ph = R(tr,p+16,j) + inc * rel`` (mod 2^32),
+    value ``(A' * SIN[ph >> 20]) >> 15`` with ``SIN[k] = round(32767 sin(2 pi k / 4096))``, where ``j`` is the
+    partial's note index and ``rel`` the sample's offset in that note:
+      - generator v2 (default, ``envelope=True``): every track has its own tempo,
+        ``note_len = ((sr // 4) * (12 + R(tr,40,0) % 9)) // 16`` (0.19 .. 0.31 s), every partial its own
+        onset phase ``off = (note_len * (R(tr,p+32,0) % 1024)) // 1024`` (``j = (i + off) // note_len``), and
+        every note decays linearly to half amplitude, ``A' = (A * E) >> 16`` with
+        ``E = 65536 - (rel * 32768) // note_len``, as a struck or plucked note: landmark times lock to the
+        onsets, and the instruments' independent rhythms give the landmark pairs their spread of dt;
+      - generator v0 (``envelope=False``): one grid for every track and partial, ``note_len = sr // 4``
+        (250 ms), ``j = i // note_len``, ``A' = A`` (stationary notes). On a stationary note the peak frame is
+        decided by noise, so an independent capture of the same track (another rate, another noise floor)
+        kept only ~2 % of the landmarks (DESIGN.md 4b); v0 remains for the oracle's golden fixture;
   * base noise ``R(tr,24,i) % 1137 - 568`` (about -40 dBFS rms);
   * optional query noise ``R(tr ^ salt, 25, i) % (2a+1) - a`` (``a`` from the SNR);
   * sum, clip to int16, divide by 32768.
@@ -75,23 +80,33 @@ def noise_halfwidth(snr_db: float | None) -> int:
     return int(round(rms * np.sqrt(3.0)))
 
 
+def note_params(track: int, sr: int, envelope: bool = True) -> tuple[int, list[int]]:
+    """(note_len, per-partial onset offsets) of a track (generator v2; v0: sr // 4 and zeros)."""
+    if not envelope:
+        return sr // 4, [0] * N_PARTIALS
+    note_len = ((sr // 4) * (12 + int(rnd(track, 40, 0)) % 9)) // 16
+    return note_len, [(note_len * (int(rnd(track, p + 32, 0)) % 1024)) // 1024 for p in range(N_PARTIALS)]
+
+
 def synth_int16(track: int, start: int, n: int, sr: int, noise_a: int = 0, salt: int = 0,
                 fmax_hz: int = 8000, envelope: bool = True) -> np.ndarray:
     """int32 array of int16-range samples of track ``track`` at absolute samples start..start+n."""
     if n <= 0:
         return np.zeros(0, dtype=np.int32)
-    note_len = sr // 4
+    note_len, offs = note_params(track, sr, envelope)
     inc_min, inc_rng = inc_params(sr, fmax_hz)
     i = np.arange(start, start + n, dtype=np.int64)
-    j = i // note_len
-    rel = (i - j * note_len).astype(np.uint64)
-    env = (65536 - (rel.astype(np.int64) * 32768) // note_len) if envelope else np.int64(65536)
     acc = np.zeros(n, dtype=np.int64)
     with np.errstate(over="ignore"):
         for p in range(N_PARTIALS):
+            ip = i + offs[p]
+            j = ip // note_len
+            rel = (ip - j * note_len).astype(np.uint64)
             r = rnd(track, p, j).astype(np.uint64)
             inc = (np.uint64(inc_min) + ((r * np.uint64(inc_rng)) >> np.uint64(32))) & np.uint64(0xFFFFFFFF)
-            amp = ((983 + (rnd(track, p + 8, j).astype(np.int64) % 2949)) * env) >> 16
+            amp = 983 + (rnd(track, p + 8, j).astype(np.int64) % 2949)
+            if envelope:
+                amp = (amp * (65536 - (rel.astype(np.int64) * 32768) // note_len)) >> 16
             ph = (rnd(track, p + 16, j).astype(np.uint64) + inc * rel) & np.uint64(0xFFFFFFFF)
             acc += (amp * _SIN_TABLE[(ph >> np.uint64(20)).astype(np.int64)]) >> 15
         acc += rnd(track, 24, i).astype(np.int64) % 1137 - 568

@@ -78,6 +78,15 @@ void launch_exact_consensus(const int32_t *rows, const int32_t *nrows, int mr, c
 void launch_rows_scatter(const int32_t *src, const int32_t *order, int n, int mr, int32_t *dst, hipStream_t s);
 }  // namespace aid
 
+#if defined(AID_K2_STAMPS)
+namespace aid {
+int k2_stamps_read(unsigned long long *out, bool reset);
+}
+extern "C" int aid_diag_k2_stamps(unsigned long long *out, int reset) {  // diagnostic build only
+    return aid::k2_stamps_read(out, reset != 0);
+}
+#endif
+
 using namespace aid;
 
 static thread_local std::string g_err;
@@ -807,6 +816,7 @@ int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int6
     if (!e || !dst || !tracks || !starts || n_clips < 0 || n < 0 || noise_a < 0 || sample_rate <= 0)
         return fail(AID_ERR_INVALID, "aid_synth: bad argument");
     if (flags & ~AID_SYNTH_STATIONARY) return fail(AID_ERR_INVALID, "aid_synth: unknown flags");
+    if (sample_rate > 384000) return fail(AID_ERR_INVALID, "aid_synth: sample_rate above 384 kHz");
     if (fmax_hz <= 100 || 2 * (int64_t)fmax_hz > sample_rate)
         return fail(AID_ERR_INVALID, "aid_synth: fmax_hz must be in (100, sample_rate / 2]");
     if (n_clips == 0 || n == 0) return AID_OK;

@@ -8,8 +8,13 @@
 // stably, so a bucket keeps arrival order.
 //
 // Hand-written sort (3 passes of 9-bit digits over bits 0..26, 512 digits per pass):
-//   count    per tile of kTile = 4096 postings, the digit histogram (LDS atomics) -> counts[digit][tile];
-//   scan     exclusive scan of counts in digit-major order: the global start of (digit, tile);
+//   count    per tile of kTile = 4096 postings, the digit histogram (LDS atomics) -> counts[tile][digit], one
+//            contiguous 2 KB row per tile (full lines; a digit-major matrix put each 4-B entry ~890 KB from its
+//            neighbour, one partial line per entry: 3.8 GB written for a 0.46 GB matrix, 3.6 GB re-read by the
+//            scatter);
+//   scan     the global start of (digit, tile) in digit-major order, over the tile-major matrix: column sums per
+//            group of kColTiles tiles, a column scan of those with the digit totals' exclusive scan, then
+//            each group's running column prefix (every read and write a contiguous row);
 //   scatter  a workgroup of 4 waves loads its tile (wave w: items w*1024 .. +1023, 64 consecutive per
 //            load), ranks every item stably inside the tile (ballot match per 64-item slot, wave-private
 //            running digit counters by LDS atomics issued back to back, cross-wave offsets), stages the tile
@@ -74,7 +79,7 @@ __device__ __forceinline__ uint64_t valid_lanes(int64_t i0, int64_t n) {
     return i0 + 64 <= n ? ~0ull : (i0 >= n ? 0ull : (~0ull >> (64 - (int)(n - i0))));
 }
 
-// counts[d * tiles + tile] = items of tile `tile` whose digit at `shift` is d (order does not matter here:
+// counts[tile * kDigits + d] = items of tile `tile` whose digit at `shift` is d (order does not matter here:
 // one LDS atomic per item)
 template <bool FIRST>
 __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__restrict__ keys,
@@ -106,8 +111,70 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
 #pragma unroll
     for (int j = 0; j < kDigitsPerThread; ++j) {
         const int dd = tid + j * kSortThreads;
-        counts[(int64_t)dd * tiles + tile] = c[dd];
+        counts[tile * kDigits + dd] = c[dd];
     }
+}
+
+// ---- (digit, tile) starts from the tile-major counts: offs[t][d] = sum_{d' < d} total[d'] + sum_{t' < t} counts[t'][d]
+constexpr int kColTiles = 256;  // tiles per column-sum group
+__global__ __launch_bounds__(kDigits) void k_col_sum(const uint32_t *__restrict__ counts, int64_t tiles,
+                                                     uint32_t *__restrict__ gsum) {
+    const int d = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * kColTiles, t1 = min(t0 + kColTiles, tiles);
+    uint32_t acc = 0;
+#pragma unroll 8
+    for (int64_t t = t0; t < t1; ++t) acc += counts[t * kDigits + d];
+    gsum[(int64_t)blockIdx.x * kDigits + d] = acc;
+}
+
+// one workgroup: per digit, the exclusive prefix of the group sums (goff) plus the digit's global base
+__global__ __launch_bounds__(kDigits) void k_col_scan(const uint32_t *__restrict__ gsum, int64_t groups,
+                                                      uint32_t *__restrict__ goff) {
+    __shared__ uint32_t ws[kDigits / 64];
+    const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    uint32_t run = 0;
+#pragma unroll 8
+    for (int64_t g = 0; g < groups; ++g) {
+        const uint32_t v = gsum[g * kDigits + d];
+        goff[g * kDigits + d] = run;
+        run += v;
+    }
+    uint32_t x = run;  // inclusive scan of the digit totals over the workgroup
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    uint32_t base = x - run;
+    for (int i = 0; i < w; ++i) base += ws[i];
+#pragma unroll 8
+    for (int64_t g = 0; g < groups; ++g) goff[g * kDigits + d] += base;
+}
+
+__global__ __launch_bounds__(kDigits) void k_col_apply(const uint32_t *__restrict__ counts, int64_t tiles,
+                                                       const uint32_t *__restrict__ goff, uint32_t *__restrict__ offs) {
+    const int d = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * kColTiles, t1 = min(t0 + kColTiles, tiles);
+    uint32_t run = goff[(int64_t)blockIdx.x * kDigits + d];
+#pragma unroll 8
+    for (int64_t t = t0; t < t1; ++t) {
+        const uint32_t c = counts[t * kDigits + d];
+        offs[t * kDigits + d] = run;
+        run += c;
+    }
+}
+
+static int64_t col_groups(int64_t tiles) { return (tiles + kColTiles - 1) / kColTiles; }
+
+static void digit_starts(const uint32_t *counts, int64_t tiles, uint32_t *offs, uint32_t *tmp, hipStream_t s) {
+    const int64_t groups = col_groups(tiles);
+    uint32_t *gsum = tmp, *goff = tmp + groups * kDigits;
+    hipLaunchKernelGGL(k_col_sum, dim3((unsigned)groups), dim3(kDigits), 0, s, counts, tiles, gsum);
+    hipLaunchKernelGGL(k_col_scan, dim3(1), dim3(kDigits), 0, s, (const uint32_t *)gsum, groups, goff);
+    hipLaunchKernelGGL(k_col_apply, dim3((unsigned)groups), dim3(kDigits), 0, s, counts, tiles,
+                       (const uint32_t *)goff, offs);
 }
 
 template <bool FIRST, bool LAST>
@@ -135,7 +202,7 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
 #pragma unroll
     for (int j = 0; j < kDigitsPerThread; ++j) {
         const int dd = tid + j * kSortThreads;
-        g_start[dd] = offs[(int64_t)dd * tiles + tile];
+        g_start[dd] = offs[tile * kDigits + dd];
     }
     uint32_t key[kSlots];
     uint64_t val[kSlots];
@@ -381,7 +448,8 @@ int64_t radix_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 // scratch of the sort build in u32 units: the tile counts, their scan, and the scans' temporaries
 size_t radix_scratch_u32(int64_t n) {
     const int64_t c = (int64_t)kDigits * radix_tiles(n);
-    return (size_t)(2 * c) + std::max(scan8_tmp(c), scan8_tmp((int64_t)(1u << 26) + 1)) + 64;
+    return (size_t)(2 * c) +
+           std::max<size_t>(2 * (size_t)kDigits * col_groups(radix_tiles(n)), scan8_tmp((int64_t)(1u << 26) + 1)) + 64;
 }
 
 // temporary storage of the rocPRIM sort for n pairs
@@ -424,18 +492,18 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
         // pass 1: SoA postings -> (keys1, vals1); pass 2: -> (keys0, vals0); pass 3: -> (keys1, vals1)
         const dim3 g((unsigned)tiles), b(kSortThreads);
         timed_launch(k_radix_count<true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
-        scan8<false>(counts, offs, c, stmp, s);
+        digit_starts(counts, tiles, offs, stmp, s);
         timed_launch(k_radix_scatter<true, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt, tomb,
                      n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
-        scan8<false>(counts, offs, c, stmp, s);
+        digit_starts(counts, tiles, offs, stmp, s);
         timed_launch(k_radix_scatter<false, false>, g, b, 0, s, (const uint32_t *)keys1, (const uint64_t *)vals1,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
                      kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0, (uint32_t *)nullptr);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys0, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, counts, tiles);
-        scan8<false>(counts, offs, c, stmp, s);
+        digit_starts(counts, tiles, offs, stmp, s);
         timed_launch(k_radix_scatter<false, true>, g, b, 0, s, (const uint32_t *)keys0, (const uint64_t *)vals0,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
                      2 * kDigitBits, (const uint32_t *)offs, tiles, (uint32_t *)nullptr, vals1, E);

@@ -33,6 +33,16 @@ namespace aid {
 
 constexpr int kRowsPerStep = 4;
 
+#if defined(AID_K2_STAMPS)
+// Diagnostic build only (build_ext.build(variant=..., defines=("AID_K2_STAMPS",)), probes/k2_stamps_probe.py): each
+// surviving wave sums s_memtime cycles per segment of its 4-row steps and adds them here at its end:
+// [0] wait at the step's first barrier (the other waves still on the previous rows), [1] wait for the step's row
+// loads, [2] staging (keys + LDS writes + next loads), [3] wait at the staging barrier, [4] the 4 rows' window
+// logic and mask emission, [5] surviving waves, [6] their whole lives (entry to end), [7] strip-cold (exiting) waves
+__device__ unsigned long long g_k2_stamps[8];
+#define AID_K2_T() ((unsigned long long)__builtin_amdgcn_s_memtime())
+#endif
+
 // Peak decisions compare powers as int32 keys: a power is >= +0 (never -0: FPSPEC 4's
 // fma(Xr, Xr, Xi*Xi), stored unscaled as 4P by K1), and non-negative binary32 values order exactly like their bit
 // patterns. NaN maps to key 0, which reproduces the oracle's `row > l ? row : l` maxima (a NaN
@@ -63,6 +73,10 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
     // wave = the 256-bin quarter of the row this wave owns, rotated by the workgroup index: the
     // waves of a workgroup go to the CU's 4 SIMDs in order, so without rotation every workgroup's
     // low-frequency (hot) quarter lands on SIMD 0 and its cold top quarter on SIMD 3
+#if defined(AID_K2_STAMPS)
+    const unsigned long long st_birth = AID_K2_T();
+    unsigned long long st_seg[5] = {0, 0, 0, 0, 0}, st_mark = st_birth;
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(((int)(threadIdx.x >> 6) + (int)blockIdx.x) & 3);
     const int tid = wave * 64 + lane;  // owner of bins 4 tid .. 4 tid + 3
@@ -164,6 +178,9 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
             // zeroed LDS bins are written before it ends. The cold waves are counted (64 counters, read
             // and reset by K3) so the host can size the next call's strips (extract_locked)
             if (lane == 0 && cold_cnt) atomicAdd(&cold_cnt[blockIdx.x & 63], 1u);
+#if defined(AID_K2_STAMPS)
+            if (lane == 0) atomicAdd(&g_k2_stamps[7], 1ull);
+#endif
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             return;
         }
@@ -196,7 +213,15 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
             const int it = base + s;
             if (it >= iters) break;  // workgroup-uniform
             if (s % kRowsPerStep == 0) {
+#if defined(AID_K2_STAMPS)
+                { const unsigned long long t = AID_K2_T(); st_seg[4] += t - st_mark; st_mark = t; }
+                if (it > 0) __syncthreads();
+                { const unsigned long long t = AID_K2_T(); st_seg[0] += t - st_mark; st_mark = t; }
+                __builtin_amdgcn_s_waitcnt(0x0070 | 0x0F00);  // vmcnt(0): the step's row loads (diagnostic only)
+                { const unsigned long long t = AID_K2_T(); st_seg[1] += t - st_mark; st_mark = t; }
+#else
                 if (it > 0) __syncthreads();  // every wave is done with the previous 4 rows
+#endif
                 // stage rows it .. it+3 as keys, then fetch rows it+PF .. (register staging beats
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
 #pragma unroll
@@ -212,7 +237,13 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                     pf[slot] = load_row(rn, it + j + kRowsPerStep < iters ? hsave[j] : 0ull);
                 }
                 hwv = hotwords(rbeg + it + 2 * kRowsPerStep);
+#if defined(AID_K2_STAMPS)
+                { const unsigned long long t = AID_K2_T(); st_seg[2] += t - st_mark; st_mark = t; }
                 __syncthreads();
+                { const unsigned long long t = AID_K2_T(); st_seg[3] += t - st_mark; st_mark = t; }
+#else
+                __syncthreads();
+#endif
             }
             const int r = rbeg + it;
             bool pk[4];
@@ -301,7 +332,29 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
             }
         }
     }
+#if defined(AID_K2_STAMPS)
+    {
+        const unsigned long long t = AID_K2_T();
+        st_seg[4] += t - st_mark;
+        if (lane == 0) {
+            for (int k = 0; k < 5; ++k) atomicAdd(&g_k2_stamps[k], st_seg[k]);
+            atomicAdd(&g_k2_stamps[5], 1ull);
+            atomicAdd(&g_k2_stamps[6], t - st_birth);
+        }
+    }
+#endif
 }
+
+#if defined(AID_K2_STAMPS)
+int k2_stamps_read(unsigned long long *out, bool reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
+    if (reset) {
+        const unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_k2_stamps), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
 
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
                       float thr, const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {

@@ -26,7 +26,8 @@ struct SynthParams {
     int32_t noise_a;    // query noise half-width (0 = none)
     uint32_t salt;
     uint32_t seed_mul;  // (SEED * 0x9E3779B9) mod 2^32
-    int32_t envelope;   // 1: each note decays linearly to half amplitude (generator v2); 0: stationary notes (v0)
+    int32_t envelope;   // 1: generator v2 (per-track tempo, per-partial onsets, decaying notes); 0: v0 (stationary,
+                        // one 250 ms grid)
 };
 
 __global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, const uint32_t *__restrict__ tracks,
@@ -40,16 +41,22 @@ __global__ __launch_bounds__(256) void k_synth(float *__restrict__ out, const ui
     const uint32_t tr = tracks[c];
     const int64_t i = starts[c] + i_local;
     const uint32_t key = mix32(tr + sp.seed_mul);
-    const int64_t j = i / sp.note_len;
-    const uint32_t rel = (uint32_t)(i - j * sp.note_len);
-    // note envelope (Q16): 65536 at the onset down to ~32768 at the note's end
-    const int32_t env = sp.envelope ? 65536 - (int32_t)((rel * 32768u) / (uint32_t)sp.note_len) : 65536;
+    // generator v2 (aidfp/synth.py): the track's tempo and each partial's onset phase; v0: one 250 ms grid
+    const uint32_t nl = sp.envelope ? ((uint32_t)sp.note_len * (12u + rnd(key, 40, 0) % 9u)) / 16u : (uint32_t)sp.note_len;
+    // sample indices below 2^31 take 32-bit divisions (a 64-bit one is a long software sequence)
+    const bool narrow = i + (int64_t)nl < 0x80000000ll;
     int32_t acc = 0;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
+        const uint32_t off = sp.envelope ? (uint32_t)(((uint64_t)nl * (rnd(key, p + 32, 0) % 1024u)) >> 10) : 0u;
+        const int64_t ip = i + off;
+        const int64_t j = narrow ? (int64_t)((uint32_t)ip / nl) : ip / (int64_t)nl;
+        const uint32_t rel = (uint32_t)(ip - j * (int64_t)nl);
         const uint32_t r = rnd(key, p, (uint32_t)j);
         const uint32_t inc = sp.inc_min + (uint32_t)(((uint64_t)r * sp.inc_rng) >> 32);
-        const int32_t amp = ((983 + (int32_t)(rnd(key, p + 8, (uint32_t)j) % 2949u)) * env) >> 16;
+        int32_t amp = 983 + (int32_t)(rnd(key, p + 8, (uint32_t)j) % 2949u);
+        // note envelope (Q16): 65536 at the onset down to ~32768 at the note's end
+        if (sp.envelope) amp = (amp * (65536 - (int32_t)((rel * 32768u) / nl))) >> 16;  // rel < nl < 2^17
         const uint32_t ph = rnd(key, p + 16, (uint32_t)j) + inc * rel;
         acc += (amp * (int32_t)sin_tab[ph >> 20]) >> 15;
     }
