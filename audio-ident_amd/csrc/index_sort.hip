@@ -42,7 +42,10 @@ constexpr int kDigits = 1 << kDigitBits;
 constexpr int kSortPasses = 3;
 constexpr int kSortThreads = 256;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr int kSlots = 16;                      // 64-item slots per wave
+#ifndef AID_K4_SLOTS
+#define AID_K4_SLOTS 16  // A/B builds only (build_ext variant defines)
+#endif
+constexpr int kSlots = AID_K4_SLOTS;            // 64-item slots per wave
 constexpr int kTile = kSortThreads * kSlots;    // 4096 postings per tile
 constexpr int kDigitsPerThread = kDigits / kSortThreads;
 static_assert(kDigitBits * kSortPasses == kSortKeyBits, "passes cover the key");
@@ -81,7 +84,11 @@ __device__ __forceinline__ uint64_t valid_lanes(int64_t i0, int64_t n) {
 
 // counts[tile * kDigits + d] = items of tile `tile` whose digit at `shift` is d (order does not matter here:
 // one LDS atomic per item)
-template <bool FIRST>
+// TOMB (first pass only): a track is removed, so the key needs the posting's track and its tombstone. Without it the
+// instantiation has no dependent loads: a runtime `tomb ?` test had made hipcc wait for each slot's track load
+// before issuing the next slot's loads (16 serialised round trips per tile in the first scatter: 6.2 against 3.4 ms
+// for the other passes at 580 M postings)
+template <bool FIRST, bool TOMB = false>
 __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__restrict__ keys,
                                                               const uint32_t *__restrict__ ptrack,
                                                               const uint8_t *__restrict__ tomb, uint32_t n_tracks,
@@ -93,20 +100,23 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
     __syncthreads();
     const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
     const int64_t base = tile * kTile;
-    uint32_t d[kSlots];
+    uint32_t raw[kSlots];
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {  // all loads first
+    for (int s = 0; s < kSlots; ++s) {  // all loads first; no arithmetic on a loaded value inside the branch (hipcc
+                                        // would wait for each slot's load before issuing the next)
         const int64_t i = base + s * kSortThreads + tid;
-        d[s] = 0xFFFFFFFFu;
+        raw[s] = 0u;
         if (i < n) {
-            // the track column only when a track is removed (tomb != nullptr: uniform)
-            const uint32_t k = !FIRST ? keys[i] : tomb ? make_key(keys[i], ptrack[i], tomb, n_tracks) : bucket_key(keys[i]);
-            d[s] = (k >> shift) & (kDigits - 1);
+            // the track column only when a track is removed (TOMB)
+            raw[s] = (FIRST && TOMB) ? make_key(keys[i], ptrack[i], tomb, n_tracks) : keys[i];
         }
     }
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s)
-        if (d[s] != 0xFFFFFFFFu) atomicAdd(&c[d[s]], 1u);
+    for (int s = 0; s < kSlots; ++s) {
+        const int64_t i = base + s * kSortThreads + tid;
+        const uint32_t k = (FIRST && !TOMB) ? bucket_key(raw[s]) : raw[s];
+        if (i < n) atomicAdd(&c[(k >> shift) & (kDigits - 1)], 1u);
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kDigitsPerThread; ++j) {
@@ -116,7 +126,10 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
 }
 
 // ---- (digit, tile) starts from the tile-major counts: offs[t][d] = sum_{d' < d} total[d'] + sum_{t' < t} counts[t'][d]
-constexpr int kColTiles = 256;  // tiles per column-sum group
+#ifndef AID_K4_COLTILES
+#define AID_K4_COLTILES 256  // A/B builds only
+#endif
+constexpr int kColTiles = AID_K4_COLTILES;  // tiles per column-sum group
 __global__ __launch_bounds__(kDigits) void k_col_sum(const uint32_t *__restrict__ counts, int64_t tiles,
                                                      uint32_t *__restrict__ gsum) {
     const int d = threadIdx.x;
@@ -177,7 +190,7 @@ static void digit_starts(const uint32_t *counts, int64_t tiles, uint32_t *offs, 
                        (const uint32_t *)goff, offs);
 }
 
-template <bool FIRST, bool LAST>
+template <bool FIRST, bool LAST, bool TOMB = false>
 __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
                                                                 const uint64_t *__restrict__ vals_in,
                                                                 const uint32_t *__restrict__ ptrack,
@@ -212,7 +225,9 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
         if (i < n) {
             if (FIRST) {
                 const uint32_t tr = ptrack[i];
-                key[s] = make_key(keys_in[i], tr, tomb, n_tracks);
+                // without tombstones the raw hash is loaded here and permuted after the loop: any arithmetic on a
+                // loaded value inside this per-slot branch makes hipcc wait for that load before the next slot's
+                key[s] = TOMB ? make_key(keys_in[i], tr, tomb, n_tracks) : keys_in[i];
                 val[s] = (uint64_t)tr | ((uint64_t)pt[i] << 32);
             } else {
                 key[s] = keys_in[i];
@@ -222,6 +237,10 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
             key[s] = 0xFFFFFFFFu;
             val[s] = 0;
         }
+    }
+    if (FIRST && !TOMB) {  // past-the-end slots get some key too: they are never ranked or staged (valid_lanes)
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) key[s] = bucket_key(key[s]);
     }
     __syncthreads();  // counters zeroed
     // stable rank inside the wave: slot by slot in item order, lanes in lane order. The leader of each digit
@@ -491,10 +510,17 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
         uint32_t *counts = scratch, *offs = scratch + c;
         // pass 1: SoA postings -> (keys1, vals1); pass 2: -> (keys0, vals0); pass 3: -> (keys1, vals1)
         const dim3 g((unsigned)tiles), b(kSortThreads);
-        timed_launch(k_radix_count<true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
-        digit_starts(counts, tiles, offs, stmp, s);
-        timed_launch(k_radix_scatter<true, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt, tomb,
-                     n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
+        if (tomb) {
+            timed_launch(k_radix_count<true, true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
+            digit_starts(counts, tiles, offs, stmp, s);
+            timed_launch(k_radix_scatter<true, false, true>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
+                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
+        } else {
+            timed_launch(k_radix_count<true, false>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
+            digit_starts(counts, tiles, offs, stmp, s);
+            timed_launch(k_radix_scatter<true, false, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
+                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
+        }
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
         digit_starts(counts, tiles, offs, stmp, s);

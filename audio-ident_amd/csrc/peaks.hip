@@ -35,10 +35,10 @@ constexpr int kRowsPerStep = 4;
 
 #if defined(AID_K2_STAMPS)
 // Diagnostic build only (build_ext.build(variant=..., defines=("AID_K2_STAMPS",)), probes/k2_stamps_probe.py): each
-// surviving wave sums s_memtime cycles per segment of its 4-row steps and adds them here at its end:
-// [0] wait at the step's first barrier (the other waves still on the previous rows), [1] wait for the step's row
-// loads, [2] staging (keys + LDS writes + next loads), [3] wait at the staging barrier, [4] the 4 rows' window
-// logic and mask emission, [5] surviving waves, [6] their whole lives (entry to end), [7] strip-cold (exiting) waves
+// surviving wave sums s_memtime cycles spent at the step's first barrier (waiting for the other waves of its
+// workgroup to finish the previous 4 rows) and adds them here at its end. Two s_memtime per step, their
+// difference taken a step later (no extra wait in the row logic). [0] barrier wait, [5] surviving waves,
+// [6] their whole lives (entry to end), [7] strip-cold (exiting) waves; [1..4] unused
 __device__ unsigned long long g_k2_stamps[8];
 #define AID_K2_T() ((unsigned long long)__builtin_amdgcn_s_memtime())
 #endif
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
     // low-frequency (hot) quarter lands on SIMD 0 and its cold top quarter on SIMD 3
 #if defined(AID_K2_STAMPS)
     const unsigned long long st_birth = AID_K2_T();
-    unsigned long long st_seg[5] = {0, 0, 0, 0, 0}, st_mark = st_birth;
+    unsigned long long st_bar = 0, st_b0 = 0, st_b1 = 0;
 #endif
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(((int)(threadIdx.x >> 6) + (int)blockIdx.x) & 3);
@@ -214,11 +214,10 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
             if (it >= iters) break;  // workgroup-uniform
             if (s % kRowsPerStep == 0) {
 #if defined(AID_K2_STAMPS)
-                { const unsigned long long t = AID_K2_T(); st_seg[4] += t - st_mark; st_mark = t; }
+                st_bar += st_b1 - st_b0;  // the previous step's barrier wait (its stamps have long arrived)
+                st_b0 = AID_K2_T();
                 if (it > 0) __syncthreads();
-                { const unsigned long long t = AID_K2_T(); st_seg[0] += t - st_mark; st_mark = t; }
-                __builtin_amdgcn_s_waitcnt(0x0070 | 0x0F00);  // vmcnt(0): the step's row loads (diagnostic only)
-                { const unsigned long long t = AID_K2_T(); st_seg[1] += t - st_mark; st_mark = t; }
+                st_b1 = AID_K2_T();
 #else
                 if (it > 0) __syncthreads();  // every wave is done with the previous 4 rows
 #endif
@@ -237,13 +236,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                     pf[slot] = load_row(rn, it + j + kRowsPerStep < iters ? hsave[j] : 0ull);
                 }
                 hwv = hotwords(rbeg + it + 2 * kRowsPerStep);
-#if defined(AID_K2_STAMPS)
-                { const unsigned long long t = AID_K2_T(); st_seg[2] += t - st_mark; st_mark = t; }
                 __syncthreads();
-                { const unsigned long long t = AID_K2_T(); st_seg[3] += t - st_mark; st_mark = t; }
-#else
-                __syncthreads();
-#endif
             }
             const int r = rbeg + it;
             bool pk[4];
@@ -335,9 +328,9 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
 #if defined(AID_K2_STAMPS)
     {
         const unsigned long long t = AID_K2_T();
-        st_seg[4] += t - st_mark;
+        st_bar += st_b1 - st_b0;
         if (lane == 0) {
-            for (int k = 0; k < 5; ++k) atomicAdd(&g_k2_stamps[k], st_seg[k]);
+            atomicAdd(&g_k2_stamps[0], st_bar);
             atomicAdd(&g_k2_stamps[5], 1ull);
             atomicAdd(&g_k2_stamps[6], t - st_birth);
         }

@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tracks", type=int, default=100000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--modes", default="radix,rocprim,atomic,radix_again",
+                    help="builds to time, of radix, rocprim, atomic, radix_again (AIDFP_LIB picks an A/B library)")
     args = ap.parse_args()
     import torch
 
@@ -32,9 +34,13 @@ def main():
     torch.cuda.set_device(0)
     eng = Engine(44100, device=0)
     st = ingest_synthetic(eng, np.arange(args.tracks, dtype=np.uint32), 30.0, batch=1024)
-    out = {"postings": st.postings_total}
+    import os
+
+    out = {"postings": st.postings_total, "library": os.environ.get("AIDFP_LIB", "product")}
     ref = None
-    for name, mode in (("radix", 1), ("rocprim", 3), ("atomic", 2), ("radix_again", 1)):
+    modes = [m for m in (("radix", 1), ("rocprim", 3), ("atomic", 2), ("radix_again", 1))
+             if m[0] in args.modes.split(",")]
+    for name, mode in modes:
         eng.force("k4_build", mode)
         times, ev = [], []
         for _ in range(args.reps):
@@ -57,6 +63,8 @@ def main():
                      "bytes_per_posting_at_event_time": None}
     n = st.postings_total
     for name in ("radix", "rocprim"):
+        if name not in out:
+            continue
         best = min(out[name]["event_ms"])
         out[name]["best_event_ms"] = best
         out[name]["gb_per_s_at_92B" if name == "radix" else "gb_per_s_at_125B"] = round(

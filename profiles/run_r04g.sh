@@ -12,4 +12,5 @@ mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/fetch -o run --output-format csv -- python3 probes/k4_probe.py --reps 1 > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/write -o run --output-format csv -- python3 probes/k4_probe.py --reps 1 > $OUT/write.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d gpurun_out/r04g/match -o run --output-format csv -- python3 bench_match.py --no-cpu --category-queries 200 > gpurun_out/r04g/match.json 2> gpurun_out/r04g/match.err
+timeout -k 10 200 python3 probes/k2_stamps_probe.py > gpurun_out/r04g/k2_stamps.json 2> gpurun_out/r04g/k2_stamps.err
 echo done
