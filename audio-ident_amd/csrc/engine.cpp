@@ -1851,8 +1851,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         e->st_votes += h_votes[q];
         e->st_records += h_count[q];
     }
-    if (speculate)
-        for (int q = 0; q < nq; ++q) e->st_post_reads += h_votes[q];  // the LDS path ran every query once
+    if (speculate)  // the LDS path ran every query once: two enumerations (counting, then the exact inserts)
+        for (int q = 0; q < nq; ++q) e->st_post_reads += 2 * h_votes[q];
     // global histogram, sized for the votes that pass K5a's 2^20-bit seen filter (all but the
     // distinct bits: v - m(1 - e^{-v/m})) at ~2 per bucket: a chance bucket reaching
     // min_match - 1 then has probability ~1e-5. Sizing it for ALL votes (2 buckets each: 2 MB rows on
@@ -1866,11 +1866,16 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     const double fwd = parts * (vp - m_seen * (1.0 - std::exp(-vp / m_seen)));
     int bits = 15;
     while (bits < 24 && (double)(1ull << bits) < fwd / kForwardedPerBucket) ++bits;
-    // LDS fast path only while its 2^16 counters stay sparse (2 buckets per expected vote). It is
-    // exact for heavier queries too (overflows fall back; tests/test_gpu_match_load.py) but one
-    // query per CU cannot keep enough posting reads in flight: config 4's 33k windows (~540k
-    // votes each) took 48.6 s on it against 1.43 s on the global path
-    const bool fast = !speculate && (e->k5_path == 1 || (e->k5_path == 0 && 2.0 * votes <= 65536.0));
+    // LDS fast path while its 2^16 counters stay sparse enough. It is exact for heavier queries too (overflows
+    // fall back; tests/test_gpu_match_load.py) but one query per CU cannot keep enough posting reads in flight:
+    // round-1 config 4 (v0 catalog, ~540k votes per window) took 48.6 s on it against 1.43 s on the global path.
+    // On the v2 catalog (~84.5k votes per window, probes/k5_path_probe.py) it is the faster path (201k against
+    // 185k clips/s, rows equal), so a batch goes to it when its mean query has <= 2^17 votes (2 per counter) and
+    // none has more than 2^20 (a heavier one falls back to the global path after its LDS run)
+    double vsum = 0.0;
+    for (int q = 0; q < nq; ++q) vsum += (double)h_votes[q];
+    const bool lds_load = 2.0 * votes <= 65536.0 || (vsum / std::max(nq, 1) <= (double)(1 << 17) && votes <= (double)(1 << 20));
+    const bool fast = !speculate && (e->k5_path == 1 || (e->k5_path == 0 && lds_load));
     // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
     // through to the global-histogram path below
     if (fast) {
@@ -1892,7 +1897,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         }
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();
-        for (int q = 0; q < nq; ++q) e->st_post_reads += h_votes[q];
+        for (int q = 0; q < nq; ++q) e->st_post_reads += 2 * h_votes[q];  // counting pass + insert pass
         e->st_q_lds += nq;
     }
     if (speculate) e->st_q_lds += nq;

@@ -488,7 +488,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
             "frac": round(alg / k5_s / 1e9 / PEAK, 4) if k5_s else None,
             "per_kernel_ms": {k: round(prof[k][0], 3) for k in K5_KERNELS if k in prof and prof[k][1]},
             "source": "rank 0, untimed second pass of the same clips with HIP events on the K5 kernels",
-            "note": "bytes = 8 B x postings K5 read (LDS path once per vote, global path once per K5a key partition "
+            "note": "bytes = 8 B x postings K5 read (LDS path twice per vote (counting and insert passes), global path once per K5a key partition "
                     "+ once in K5b) + 8 B x query records; the vote histogram's atomics and the exact tables stay "
                     "in LDS / the caches and are not counted"}
     return {"value": round(world * n / t_max, 1), "unit": "clips/s", "clips_per_rank": n, "positives_per_rank": n_pos,

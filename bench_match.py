@@ -307,7 +307,7 @@ def lane(args, eng, st, truth, starts, n_pos, n_neg, t_index) -> int:
                 "achieved": round((post_bytes + 8 * ms["records"]) / k5_s / 1e9, 1) if k5_s else None,
                 "frac": round((post_bytes + 8 * ms["records"]) / k5_s / 1e9 / HBM_PEAK_GBS, 4) if k5_s else None,
                 "k5_seconds": round(k5_s, 4),
-                "note": "bytes = 8 B x postings K5 read (a vote reads one 8-B posting per pass: LDS path once, "
+                "note": "bytes = 8 B x postings K5 read (a vote reads one 8-B posting per pass: LDS path twice, "
                         "global path once per K5a key partition + once in K5b) + 8 B x query records; the "
                         "vote histogram's random atomics and the exact table stay in LDS/L2 and are not counted"}
     # robustness categories on a subset (untimed)

@@ -188,8 +188,8 @@ int aid_index_remove(aid_engine *e, uint32_t track);
 int aid_index_compact(aid_engine *e, int64_t *n_removed);
 int aid_index_finalize(aid_engine *e);
 /* Cumulative match counters since the last reset: out[0] queries, [1] exact votes (postings whose hash
-   a query record hits), [2] postings K5 read (LDS path: once per vote; global path: once per key
-   partition in K5a + once in K5b), [3] queries answered on the LDS path, [4] on the global path,
+   a query record hits), [2] postings K5 read (LDS path: twice per vote, its counting and insert passes;
+   global path: once per key partition in K5a + once in K5b), [3] queries answered on the LDS path, [4] on the global path,
    [5] query records. The match roofline is 8 B x out[2] / the K5 kernels' time. */
 int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset);
 /* n_postings = stored postings, n_live = postings in the built CSR (-1 if stale), n_tracks = max id + 1 */
