@@ -502,6 +502,10 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 // Phase 4: best d per track, rank, write rows (same as K5b). Any table overflow, or a
 //          16-bit counter reaching 0xFFFF, reports nrows = -1 and the host re-runs the query
 //          on the global-histogram path.
+#ifndef AID_K5_LDS_U
+#define AID_K5_LDS_U 4  // A/B builds only
+#endif
+constexpr int kLdsWindows = AID_K5_LDS_U;  // windows of 64 posting loads a wave keeps in flight (LDS path)
 constexpr int kLdsHistBits = 16;
 constexpr int kFastVoteCap = 4096;
 constexpr int kFastTrackCap = 1024;
@@ -546,7 +550,7 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
     __syncthreads();
     const bool check_wrap = L.votes >= 0xFFFFu;
     // phase 1
-    for_each_vote<4>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
+    for_each_vote<kLdsWindows>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
         const uint32_t h = mix_td(tr, d) & hmask;
         if (check_wrap) {
             const uint32_t old = atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
     }
     __syncthreads();
     // phase 3
-    for_each_vote<4>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
+    for_each_vote<kLdsWindows>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
         const uint32_t hf = mix_td(tr, d);
         const uint32_t h = hf & hmask;
         if (!((L.hot[h >> 5] >> (h & 31)) & 1u)) return;
