@@ -257,6 +257,17 @@ class FingerprintService:
             self._names.pop(old, None)
             eng.index_remove(old)
 
+    def register_tracks(self, names: dict) -> None:
+        """Name the engine track ids of postings that were added to this service's engine directly (a bulk
+        catalog built on the device, e.g. aidfp.catalog.ingest_synthetic): `names` maps name -> track id, as
+        index_track records per store. Not journaled: call checkpoint() to persist (the bulk-ingest recipe)."""
+        with self._rw.write():
+            self._eng()
+            for name, tid in names.items():
+                self._ids[str(name)] = int(tid)
+                self._names[int(tid)] = str(name)
+            self._next = max([self._next] + [int(t) + 1 for t in names.values()])
+
     def submit_query(self, pcm: bytes):
         """Queue one query for the coalescer; returns a concurrent.futures.Future of list[OlafMatch]."""
         return self._coalescer.submit(pcm)

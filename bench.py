@@ -532,10 +532,7 @@ def service_leg(args, rank, world, dist, torch) -> dict:
             out["index"] = {"tracks": T, "track_seconds": 30.0, "source_sr": 44100, "index_sr": SSR,
                             "postings": int(st.postings_total), "build_s": round(time.perf_counter() - t, 3)}
             # the service's name maps for the catalog (what index_track would have recorded per store)
-            with svc._rw.write():
-                svc._ids = {f"track-{i}": i for i in range(T)}
-                svc._names = {i: f"track-{i}" for i in range(T)}
-                svc._next = T
+            svc.register_tracks({f"track-{i}": i for i in range(T)})
             rng = np.random.default_rng(77 + rank)
             truth = rng.integers(0, T, n_req).astype(np.uint32)
             starts = rng.integers(0, 25 * QSR, n_req).astype(np.int64)

@@ -489,3 +489,17 @@ def test_coalescer_caps_batch_bytes():
     c.close()
     assert all(sum(b) <= 100 or len(b) == 1 for b in seen)
     assert [300] in seen
+
+
+def test_register_tracks_names_a_bulk_catalog(svc, tmp_path):
+    """Postings added to the service's engine directly (a device-built catalog) answer olaf_query under the names
+    register_tracks gives them, new stores take the next free id, and a checkpoint persists the names."""
+    eng = svc._eng()
+    recs = eng.extract_host([np.full(16000, 0.25, np.float32)])[0]
+    eng.index_add_records(7, recs)
+    svc.register_tracks({"bulk-7": 7})
+    assert svc.query(_pcm_of(0.25))[0].reference_path == "bulk-7"
+    assert svc.index_track(_pcm_of(0.35), "next") and svc._ids["next"] == 8
+    svc.checkpoint()
+    again = fp.FingerprintService(tmp_path / "db")
+    assert again.query(_pcm_of(0.25))[0].reference_path == "bulk-7"
