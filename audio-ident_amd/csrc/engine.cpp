@@ -1606,7 +1606,9 @@ int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_to
     hipStream_t s = e->own_stream;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     const int W = c->world;
-    if (e->g_meta.n < 2 * (size_t)W + 2) return fail(AID_ERR_STATE, "aid_index_allgather: comm not made for this engine");
+    // aid_comm_create reserved this engine's meta buffer; a comm made with another engine gets it here (16 B per
+    // rank: returning early instead would leave the other ranks blocked in the first all-gather)
+    HIP_TRY(e->g_meta.reserve(2 * (size_t)W + 2));
     // Every rank runs the same collectives whatever happens locally: (1) (count, n_tracks), (2) one ok flag
     // per rank after every step that can fail locally, (3) the payload only when every rank is ready. A
     // rank-local failure (bad arguments, OOM of the exchange buffers or the grown index, the pack) is
