@@ -253,3 +253,45 @@ def test_sort_build_equals_atomic_build():
         assert np.array_equal(a, b), f"query {q}: rows differ between the builds"
         assert not np.isin(b[:, 1] if len(b) else [], [tracks[4], tracks[10]]).any()
 
+
+
+@pytest.mark.parametrize("removed", [False, True])
+def test_sort_build_many_column_groups(removed):
+    """The radix build over more than one column-scan group (> 256 tiles of 4096 postings, ~1.4 M postings here), with
+    and without tombstones (the templated first pass): rows equal rocPRIM's build for 48 queries."""
+    import torch
+
+    n = SR * 12
+    tracks = np.arange(600, dtype=np.uint32) * 3 + 1
+    rng = np.random.default_rng(11)
+    pick = rng.choice(len(tracks), 48, replace=False)
+    qs = [synth.synth(int(tracks[i]), int(rng.integers(0, 7 * SR)), 5 * SR, SR, snr_db=20.0, salt=60 + int(i))
+          for i in pick]
+    recs = [O.fingerprint(q, HOP) for q in qs]
+    out = {}
+    for mode in ("sort", "rocprim"):
+        eng = Engine(SR)
+        try:
+            eng.force("k4_build", {"sort": 1, "rocprim": 3}[mode])
+            pcm = torch.empty(200 * n, dtype=torch.float32, device="cuda")
+            for b0 in range(0, len(tracks), 200):
+                tr = tracks[b0:b0 + 200]
+                eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n)
+                eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n)
+                eng.index_add_extracted(tr)
+            if removed:
+                for i in pick[:5]:
+                    eng.index_remove(int(tracks[i]))
+            eng.index_finalize()
+            st = eng.index_stats()
+            assert st["postings"] > 256 * 4096
+            out[mode] = (st, eng.query(recs))
+        finally:
+            eng.close()
+    (ss, rs), (sr, rr) = out["sort"], out["rocprim"]
+    assert ss == sr
+    assert all(np.array_equal(a, b) for a, b in zip(rs, rr))
+    hits = [int(r[0, 1]) if len(r) else None for r in rs]
+    gone = {int(tracks[i]) for i in pick[:5]} if removed else set()
+    assert sum(h == int(tracks[i]) for h, i in zip(hits, pick) if int(tracks[i]) not in gone) >= 40
+    assert not any(h in gone for h in hits if h is not None)
