@@ -82,6 +82,23 @@ __device__ __forceinline__ void pstore(float *p, float v) {
 // and (Z[768 - k], Z[1024 - k]) as one ds_read_b128 each (8 per frame; stage-C writers and both readers
 // conflict-free, checked exhaustively). Lane 0's unit-0 mirror read lands on a copy of Z[768] at slot 1026,
 // written by lane 3 of stage C.
+// PCM ring loads are non-temporal: K1 reads each sample once, and streaming it past the caches leaves the Infinity
+// Cache to the hot power rows K2 reads next (K2 -2 %, step -0.8 %, K1 unchanged in a 3-round same-box A/B,
+// profiles/r04q_k1_ntload_ab.txt). AID_K1_NTLOAD=0 (A/B builds only) restores plain loads
+#ifndef AID_K1_NTLOAD
+#define AID_K1_NTLOAD 1
+#endif
+#if AID_K1_NTLOAD
+typedef float aid_f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 pcm_nt(const float2 &r) {
+    const aid_f2v v = __builtin_nontemporal_load(reinterpret_cast<const aid_f2v *>(&r));
+    return make_float2(v.x, v.y);
+}
+#define AID_PCM(ref) pcm_nt(ref)
+#else
+#define AID_PCM(ref) (ref)
+#endif
+
 __device__ __forceinline__ int e3q_slot(int k) { return 4 * (k & 255) + ((k >> 8) ^ (2 * ((k >> 3) & 1))); }
 
 template <bool LOGMAG, int ROWS>
@@ -167,7 +184,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
 
     float2 ring[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) ring[r] = src[64 * r];
+    for (int r = 0; r < 16; ++r) ring[r] = AID_PCM(src[64 * r]);
     // the segment's first frame needs the whole ring anyway: wait for it here, so the frame loop's
     // header does not inherit this path's pending loads (hipcc's wait at the header, merged over both
     // edges, was vmcnt(1): every 4 frames the wave also waited for the previous frame's 17 stores)
@@ -200,7 +217,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
                     const int fn = min(f + 1, nfr - 1);
 #pragma unroll
                     for (int j = 0; j < ROWS; ++j)
-                        ring[(ROWS * p + j) & 15] = src[(int64_t)fn * HOP2 + 64 * (16 - ROWS + j)];
+                        ring[(ROWS * p + j) & 15] = AID_PCM(src[(int64_t)fn * HOP2 + 64 * (16 - ROWS + j)]);
                 }
                 // stage A: lane = n2
                 dft16(v, t16);
