@@ -73,8 +73,16 @@ __device__ __forceinline__ uint64_t group16(uint64_t m) {
 }
 
 // power-row store, non-temporal (streaming): K1 0.268 -> 0.266 ms, K2 0.134 -> 0.130 ms same-box (r02)
+// (AID_K1_NTSTORE=0, A/B builds only: plain stores)
+#ifndef AID_K1_NTSTORE
+#define AID_K1_NTSTORE 1
+#endif
 __device__ __forceinline__ void pstore(float *p, float v) {
+#if AID_K1_NTSTORE
     __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
 }
 
 // E3 slot of Z[k] = 4 (k & 255) + (j2 ^ 2 h), j2 = k >> 8, h = bit 3 of k: the four Z[k + 256 j2] sit in one
