@@ -78,7 +78,7 @@ class Engine:
 
     FORCE = {"k5_path": L.AID_FORCE_K5_PATH, "k5_parts": L.AID_FORCE_K5_PARTS, "k5_batch": L.AID_FORCE_K5_BATCH,
              "k2_strips_x100": L.AID_FORCE_K2_STRIPS_X100, "k4_build": L.AID_FORCE_K4_BUILD,
-             "exchange_fail": L.AID_FORCE_EXCHANGE_FAIL}
+             "exchange_fail": L.AID_FORCE_EXCHANGE_FAIL, "lane_gather": L.AID_FORCE_LANE_GATHER}
 
     def force(self, what: str, value: int) -> None:
         """Test hook (aid_engine_force): pin one of the engine's own code paths, e.g. force("k5_path", 2)."""
@@ -106,7 +106,7 @@ class Engine:
         return [self.hashes(c) for c in range(len(arrs))]
 
     def extract_device(self, pcm_ptr: int, offsets: np.ndarray, stream: int | None = None) -> None:
-        """Asynchronous extraction of device PCM; offsets = host int64[n_clips+1] (even)."""
+        """Asynchronous extraction of device PCM; offsets = host int64[n_clips+1] (odd offsets allowed)."""
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         check(self._lib.aid_extract(self._h, ctypes.c_void_p(pcm_ptr), _p(offsets), len(offsets) - 1,
                                     AID_PCM_DEVICE, ctypes.c_void_p(stream) if stream else None))

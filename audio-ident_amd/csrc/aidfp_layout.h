@@ -77,7 +77,7 @@ inline int64_t hash_capacity(int64_t F) { return kFan * peak_capacity(F); }
 
 // Per-clip descriptor uploaded with each extraction call (struct of 8 x int64).
 struct ClipDesc {
-    int64_t pcm_off;     // first sample of the clip in the PCM buffer (even)
+    int64_t pcm_off;     // first sample of the clip in the PCM buffer (odd: 4-byte aligned float2 loads)
     int64_t frames;      // F
     int64_t frame_base;  // first row of the clip in the power plane / mask plane
     int64_t strip_base;  // first K2 strip of the clip

@@ -222,6 +222,7 @@ struct aid_engine {
     int64_t k1_slots = 1;  // resident K1 waves (CUs x kStftWaves: one K1 workgroup per CU)
     int k5_path = 0;       // aid_engine_force K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int k5_parts = 0;      // aid_engine_force K5_PARTS: K5a key partitions per query (0 = by vote count)
+    int lane_gather = 0;           // aid_engine_force LANE_GATHER: stage the exact lane's sub-windows (A/B)
     int inject_exchange_fail = 0;  // aid_engine_force EXCHANGE_FAIL: the next exchange's prepare step fails (tests)
     bool k5_spec_ok = true;  // the previous query batch's heaviest query fitted the LDS path (speculation gate)
     // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
@@ -518,6 +519,10 @@ int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
             if (value != 0 && value != 1) return fail(AID_ERR_INVALID, "EXCHANGE_FAIL: 0 or 1");
             e->inject_exchange_fail = value;
             return AID_OK;
+        case AID_FORCE_LANE_GATHER:
+            if (value != 0 && value != 1) return fail(AID_ERR_INVALID, "LANE_GATHER: 0 or 1");
+            e->lane_gather = value;
+            return AID_OK;
         default:
             return fail(AID_ERR_INVALID, "aid_engine_force: unknown path id");
     }
@@ -528,7 +533,7 @@ int64_t aid_num_frames(const aid_engine *e, int64_t n) { return e ? num_frames(n
 int64_t aid_hash_capacity(const aid_engine *e, int64_t n) { return e ? hash_capacity(num_frames(n, e->cfg.hop)) : 0; }
 
 static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
-                          void *stream);
+                          void *stream, const int64_t *ends = nullptr);
 
 int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc, void *stream) {
     if (!e || !offsets || n_clips < 0) return fail(AID_ERR_INVALID, "aid_extract: bad argument");
@@ -541,9 +546,13 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
     return extract_locked(e, pcm, offsets, n_clips, loc, stream);
 }
 
+// Clip c is pcm[offsets[c], offsets[c + 1]); with `ends` (device PCM only) it is pcm[offsets[c], ends[c]), so
+// clips may overlap (the exact lane's sub-windows are read in place).
 static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
-                          void *stream) {
+                          void *stream, const int64_t *ends) {
+    if (ends && loc != AID_PCM_DEVICE) return fail(AID_ERR_INVALID, "extract: clip ends need device PCM");
     HIP_TRY(hipSetDevice(e->device));
+    auto clip_len = [&](int c) { return (ends ? ends[c] : offsets[c + 1]) - offsets[c]; };
     hipStream_t s = pick_stream(e, stream);
     const int hop = e->cfg.hop;
 
@@ -557,10 +566,12 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     }
     // a different stream than the previous call's: order against it the simple way
     if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
-    // same offsets and PCM location as the descriptors already on the device: no re-upload
-    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() == (size_t)n_clips + 3 &&
-                     e->desc_key[n_clips + 1] == loc;
-    for (int c = 0; desc_same && c <= n_clips; ++c) desc_same = e->desc_key[c] == offsets[c];
+    // same clips, PCM location and strip length as the descriptors already on the device: no re-upload
+    const size_t key_n = 2 * (size_t)n_clips + 2;
+    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() == key_n &&
+                     e->desc_key[2 * n_clips] == loc;
+    for (int c = 0; desc_same && c < n_clips; ++c)
+        desc_same = e->desc_key[2 * c] == offsets[c] && e->desc_key[2 * c + 1] == clip_len(c);
     // h_desc is rewritten below: the previous descriptor upload must have left it
     if (e->desc_ev_live) {
         HIP_TRY(hipEventSynchronize(e->desc_ev));
@@ -574,7 +585,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     // exactly one chunk, a workgroup's clip is its chunk index. Neither follows from the totals alone: a clip
     // too short for a frame has no chunk, so [short, two-chunk] also has as many chunks as clips
     bool multi_chunk = false, one_chunk_each = n_clips > 0;
-    for (int c = 0; c < n_clips; ++c) e->clip_frames[c] = num_frames(offsets[c + 1] - offsets[c], hop);
+    for (int c = 0; c < n_clips; ++c) e->clip_frames[c] = num_frames(clip_len(c), hop);
     // K2 strips per resident workgroup slot. Strip-cold K2 waves exit (peaks.hip) and their
     // registers admit more workgroups per CU (LDS allows 7 instead of the 4 of an all-hot CU): with the
     // fraction c of cold waves counted in earlier calls (K3 stores it in pinned memory; read without a sync,
@@ -590,14 +601,13 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         }
     }
     const int strip_len = peak_strip_len(e->clip_frames.data(), n_clips, std::max<int64_t>(1, (int64_t)(e->k2_slots * kx)));
-    desc_same = desc_same && e->desc_key[n_clips + 2] == strip_len;  // strip bases depend on the strip length
+    desc_same = desc_same && e->desc_key[2 * n_clips + 1] == strip_len;  // strip bases depend on the strip length
     for (int c = 0; c < n_clips; ++c) {
-        const int64_t n = offsets[c + 1] - offsets[c];
+        const int64_t n = clip_len(c);
         const int64_t F = num_frames(n, hop);
         ClipDesc &d = e->h_desc[c];
         if (loc == AID_PCM_DEVICE) {
-            if (offsets[c] & 1) return fail(AID_ERR_INVALID, "aid_extract: device clip offsets must be even");
-            d.pcm_off = offsets[c];
+            d.pcm_off = offsets[c];  // odd: K1's float2 frame loads are then 4-byte aligned (dword alignment suffices)
         } else {
             d.pcm_off = staged;
             staged += (n + 1) & ~(int64_t)1;
@@ -657,7 +667,11 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         HIP_TRY(hipMemcpyAsync(e->desc.p, e->h_desc, sizeof(ClipDesc) * n_clips, hipMemcpyHostToDevice, s));
         HIP_TRY(hipEventRecord(e->desc_ev, s));
         e->desc_ev_live = true;
-        e->desc_key.assign(offsets, offsets + n_clips + 1);
+        e->desc_key.resize(2 * (size_t)n_clips);
+        for (int c = 0; c < n_clips; ++c) {
+            e->desc_key[2 * c] = offsets[c];
+            e->desc_key[2 * c + 1] = clip_len(c);
+        }
         e->desc_key.push_back(loc);
         e->desc_key.push_back(strip_len);
         e->desc_dev_for_key = e->desc.p;
@@ -2096,8 +2110,10 @@ extern "C" int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *of
     if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
     // fan-out plan (host): clip_win = (first window, windows, mode). A window of odd length n is
     // extracted as n - 1 samples: with an even hop, frames(n) = frames(n - 1) for odd n and no
-    // frame reaches the last sample, so the records are the same and every window starts even
-    std::vector<int64_t> wdesc, xoff(1, 0);
+    // frame reaches the last sample, so the records are the same. K1 reads the windows in place
+    // (wstart / wend into the clips' PCM; at 44.1 kHz the 0.75 s window starts at an odd sample);
+    // the LANE_GATHER A/B copies them to even offsets of a staging buffer first (xoff)
+    std::vector<int64_t> wdesc, xoff(1, 0), wstart, wend;
     std::vector<int32_t> clipwin(3 * (size_t)n_clips);
     int64_t staged = 0, max_len = 0;
     for (int c = 0; c < n_clips; ++c) {
@@ -2112,6 +2128,8 @@ extern "C" int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *of
             wdesc.push_back(offsets[c] - offsets[0] + lo[w]);
             wdesc.push_back(m);
             wdesc.push_back(staged);
+            wstart.push_back(offsets[c] - offsets[0] + lo[w]);
+            wend.push_back(offsets[c] - offsets[0] + lo[w] + m);
             staged += m;
             xoff.push_back(staged);
             max_len = std::max(max_len, m);
@@ -2135,12 +2153,16 @@ extern "C" int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *of
     std::vector<int32_t> nrows(std::max(n_win, 1), 0);
     const int mr = e->cfg.max_results;
     if (n_win > 0) {
-        HIP_TRY(e->x_wdesc.reserve(wdesc.size()));
-        HIP_TRY(hipMemcpyAsync(e->x_wdesc.p, wdesc.data(), wdesc.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        HIP_TRY(e->x_win.reserve((size_t)std::max<int64_t>(staged, 2)));
-        launch_window_gather(src, e->x_wdesc.p, n_win, max_len, e->x_win.p, s);
-        HIP_TRY(hipGetLastError());
-        if (int rc = extract_locked(e, e->x_win.p, xoff.data(), n_win, AID_PCM_DEVICE, s)) return rc;
+        if (e->lane_gather) {
+            HIP_TRY(e->x_wdesc.reserve(wdesc.size()));
+            HIP_TRY(hipMemcpyAsync(e->x_wdesc.p, wdesc.data(), wdesc.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+            HIP_TRY(e->x_win.reserve((size_t)std::max<int64_t>(staged, 2)));
+            launch_window_gather(src, e->x_wdesc.p, n_win, max_len, e->x_win.p, s);
+            HIP_TRY(hipGetLastError());
+            if (int rc = extract_locked(e, e->x_win.p, xoff.data(), n_win, AID_PCM_DEVICE, s)) return rc;
+        } else {
+            if (int rc = extract_locked(e, src, wstart.data(), n_win, AID_PCM_DEVICE, s, wend.data())) return rc;
+        }
         HIP_TRY(e->q_start.reserve(n_win));
         HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), n_win * sizeof(int64_t), hipMemcpyHostToDevice, s));
         if (int rc = run_queries(e, e->records.p, e->q_start.p, e->counts.p, n_win, -1, nullptr, nrows.data(), s))

@@ -213,14 +213,26 @@ struct QueryParams {
 // would otherwise wait for it too (one L2 round trip per window). The loads are unconditional
 // (invalid lanes read post[0]) so the waits before the windows can count precisely; the record
 // of a window is found with readlane (the record index is wave-uniform), not ds_bpermute.
+// A wave takes ceil(n / (waves x rounds)) <= 64 records at a time, rounds = ceil(n / (64 waves)),
+// so the records spread evenly over every wave (config 4's windows: ~650 records, which 64-record
+// groups had left on 11 of 16 waves).
+#ifndef AID_K5_CHUNK
+#define AID_K5_CHUNK 1  // A/B builds only: 0 = 64-record groups
+#endif
 template <int U, typename G>
 __device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw,
                                                     int lane, G &&g) {
-    for (int64_t base = (int64_t)wave * 64; base < n; base += (int64_t)nw * 64) {
+#if AID_K5_CHUNK
+    const int64_t rounds = (n + (int64_t)nw * 64 - 1) / ((int64_t)nw * 64);
+    const int64_t chunk = rounds ? (n + nw * rounds - 1) / (nw * rounds) : 64;
+#else
+    const int64_t chunk = 64;
+#endif
+    for (int64_t base = (int64_t)wave * chunk; base < n; base += (int64_t)nw * chunk) {
         const int64_t i = base + lane;
         uint32_t p0 = 0, len = 0;
         int32_t tq = 0;
-        if (i < n) {
+        if (lane < chunk && i < n) {
             const uint64_t r = qp.recs[a + i];
             const uint32_t k = key26((uint32_t)r);
             tq = (int32_t)(r >> 32);
@@ -505,15 +517,29 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 #ifndef AID_K5_LDS_U
 #define AID_K5_LDS_U 4  // A/B builds only
 #endif
+// 8-bit counters (64 KB) and a 2048-entry exact table: two workgroups per CU, so one query's
+// barriers and table phases overlap another's posting reads. A counter that wraps past 255 marks
+// its bucket hot at once (>= 256 votes), as does any full counter its carry runs through, so the
+// filter stays an exact superset; with 16-bit counters (one workgroup per CU) a wrap hands the
+// query to the global path.
+#ifndef AID_K5_LDS8
+#define AID_K5_LDS8 1  // A/B builds only: 0 = 16-bit counters
+#endif
+#ifndef AID_K5_LDS_THREADS
+#define AID_K5_LDS_THREADS 1024
+#endif
 constexpr int kLdsWindows = AID_K5_LDS_U;  // windows of 64 posting loads a wave keeps in flight (LDS path)
 constexpr int kLdsHistBits = 16;
-constexpr int kFastVoteCap = 4096;
+constexpr int kLdsCtrBits = AID_K5_LDS8 ? 8 : 16;
+constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
+constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
+constexpr int kFastVoteCap = AID_K5_LDS8 ? 2048 : 4096;
 constexpr int kFastTrackCap = 1024;
-constexpr int kFastThreads = 1024;
+constexpr int kFastThreads = AID_K5_LDS_THREADS;
 
 struct FastLds {
     union {
-        uint32_t hist[(1 << kLdsHistBits) / 2];  // two 16-bit counters per word
+        uint32_t hist[(1 << kLdsHistBits) / kLdsCtrPerWord];  // packed vote counters
         struct {
             unsigned long long vkey[kFastVoteCap];
             uint32_t vcnt[kFastVoteCap], vmin[kFastVoteCap], vmax[kFastVoteCap];
@@ -526,18 +552,24 @@ struct FastLds {
     uint32_t votes;
 };
 
-__global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
-    __shared__ FastLds L;  // 136 KB: one workgroup per CU
+__global__ __launch_bounds__(kFastThreads)
+#if AID_K5_LDS8
+__attribute__((amdgpu_waves_per_eu(2 * kFastThreads / 256)))
+#endif
+void k_match_lds(QueryParams qp) {
+    __shared__ FastLds L;  // 8-bit counters: 72 KB, two workgroups per CU (16-bit: 136 KB, one)
     const int q = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = kFastThreads / 64;
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t mm = (uint32_t)qp.min_match;
     const uint32_t hmask = (1u << kLdsHistBits) - 1;
-    for (int i = tid; i < (1 << kLdsHistBits) / 2; i += kFastThreads) L.u.hist[i] = 0u;
+    for (int i = tid; i < (1 << kLdsHistBits) / kLdsCtrPerWord; i += kFastThreads) L.u.hist[i] = 0u;
+    if (AID_K5_LDS8)
+        for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
     if (tid == 0) { L.out_n = 0; L.overflow = 0; L.votes = 0; }
     __syncthreads();
-    // total votes (sum of the records' bucket lengths): below 0xFFFF no 16-bit counter can wrap,
-    // so only heavier queries pay for returning atomics (the carry check below)
+    // total votes (sum of the records' bucket lengths): below the counter maximum no counter can
+    // wrap, so only heavier queries pay for returning atomics (the carry check below)
     {
         uint32_t v = 0;
         for (int64_t i = tid; i < n; i += kFastThreads) {
@@ -548,17 +580,31 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
         if (lane == 0) atomicAdd(&L.votes, v);
     }
     __syncthreads();
-    const bool check_wrap = L.votes >= 0xFFFFu;
+    const bool check_wrap = L.votes >= kLdsCtrMax;
     // phase 1
     for_each_vote<kLdsWindows>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
         const uint32_t h = mix_td(tr, d) & hmask;
+        const uint32_t sh = kLdsCtrBits * (h % kLdsCtrPerWord);
+        uint32_t *w = &L.u.hist[h / kLdsCtrPerWord];
         if (check_wrap) {
-            const uint32_t old = atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
-            // a 16-bit counter at 0xFFFF would carry into its neighbour: hand the query to
-            // the global path (exactness over speed)
-            if (((old >> (16 * (h & 1))) & 0xFFFFu) == 0xFFFFu) L.overflow = 1;
+            const uint32_t old = atomicAdd(w, 1u << sh);
+            if (((old >> sh) & kLdsCtrMax) == kLdsCtrMax) {
+#if AID_K5_LDS8
+                // wrapped: the bucket holds >= 256 votes, so it is hot whatever its counter ends at;
+                // the carry went on into the next counters of the word, and through each full one
+                atomicOr(&L.hot[h >> 5], 1u << (h & 31));
+                for (uint32_t j = h % 4 + 1; j < 4 && ((old >> (8 * j)) & 0xFFu) == 0xFFu; ++j) {
+                    const uint32_t hj = (h & ~3u) + j;
+                    atomicOr(&L.hot[hj >> 5], 1u << (hj & 31));
+                }
+#else
+                // a 16-bit counter at 0xFFFF would carry into its neighbour: hand the query to
+                // the global path (exactness over speed)
+                L.overflow = 1;
+#endif
+            }
         } else {
-            atomicAdd(&L.u.hist[h >> 1], 1u << (16 * (h & 1)));
+            atomicAdd(w, 1u << sh);
         }
     });
     __syncthreads();
@@ -570,12 +616,14 @@ __global__ __launch_bounds__(kFastThreads) void k_match_lds(QueryParams qp) {
     for (int w = tid; w < (1 << kLdsHistBits) / 32; w += kFastThreads) {
         uint32_t bits = 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t v = L.u.hist[w * 16 + j];
-            bits |= (uint32_t)((v & 0xFFFFu) >= mm) << (2 * j);
-            bits |= (uint32_t)((v >> 16) >= mm) << (2 * j + 1);
+        for (int j = 0; j < 32 / kLdsCtrPerWord; ++j) {
+            const uint32_t v = L.u.hist[w * (32 / kLdsCtrPerWord) + j];
+#pragma unroll
+            for (int b = 0; b < kLdsCtrPerWord; ++b)
+                bits |= (uint32_t)(((v >> (kLdsCtrBits * b)) & kLdsCtrMax) >= mm) << (kLdsCtrPerWord * j + b);
         }
-        L.hot[w] = bits;
+        if (AID_K5_LDS8) L.hot[w] |= bits;  // with the buckets phase 1 found wrapped
+        else L.hot[w] = bits;
     }
     __syncthreads();
     for (int i = tid; i < kFastVoteCap; i += kFastThreads) {

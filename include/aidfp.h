@@ -101,6 +101,8 @@ int aid_engine_config(const aid_engine *e, aid_config *out);
 #define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B) */
 #define AID_FORCE_EXCHANGE_FAIL 6  /* 1: the next index exchange's pack (aid_index_pack, or the prepare step of
                                       aid_index_allgather) fails with AID_ERR_NOMEM, once (rank-failure tests) */
+#define AID_FORCE_LANE_GATHER 7    /* 1: aid_exact_lane copies its sub-windows to a staging buffer before K1 instead
+                                      of extracting them in place (A/B) */
 int aid_engine_force(aid_engine *e, int32_t what, int32_t value);
 
 /* Frames and worst-case record count of a clip of n samples (FPSPEC 1, 5). */
@@ -111,8 +113,8 @@ int64_t aid_hash_capacity(const aid_engine *e, int64_t n_samples);
  * Fingerprint extraction (K1 stft_power -> K2 peak_pick -> K3 landmark_hash).
  * Clip c is pcm[offsets[c] .. offsets[c+1]); `offsets` is a HOST array of
  * n_clips+1 non-decreasing sample indices. With AID_PCM_DEVICE, `pcm` is a device
- * pointer and every offsets[c] must be even (8-byte aligned float2 frame loads);
- * with AID_PCM_HOST the engine stages (and re-aligns) the samples itself.
+ * pointer read in place (a clip at an odd offset reads its frames with 4-byte aligned
+ * float2 loads); with AID_PCM_HOST the engine stages the samples itself.
  * Asynchronous on `stream`; results stay on the device until fetched below.
  * Replaces the FFT/peak/hash work of `olaf_c store|query` (fingerprint.py:117,185).
  */

@@ -17,11 +17,16 @@ sys.path.insert(0, str(ROOT / "audio-ident_amd"))
 sys.path.insert(0, str(ROOT))
 
 
+def reps_or1(args):
+    return max(1, args.reps)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tracks", type=int, default=100000)
     ap.add_argument("--clips", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--paths", default="auto,lds_first,global,auto_again")
     args = ap.parse_args()
     import torch
 
@@ -45,8 +50,11 @@ def main():
     offs = np.arange(n + 1, dtype=np.int64) * clip_n
     out = {"tracks": args.tracks, "clips": n}
     ref = None
-    for name, path in (("auto", 0), ("lds_first", 1), ("global", 2), ("auto_again", 0)):
+    codes = {"auto": 0, "lds_first": 1, "global": 2, "auto_again": 0, "auto_gather": 0}
+    for name in args.paths.split(","):
+        path = codes[name]
         eng.force("k5_path", path)
+        eng.force("lane_gather", int(name == "auto_gather"))  # sub-windows staged (A/B) or read in place
         eng.exact_lane(pcm_ptr=pcm.data_ptr(), offsets=offs, max_out=10)  # warm
         eng.match_stats(reset=True)
         ts = []
@@ -56,6 +64,13 @@ def main():
             rows = eng.exact_lane(pcm_ptr=pcm.data_ptr(), offsets=offs, max_out=10)
             ts.append(time.perf_counter() - t)
         ms = eng.match_stats(reset=True)
+        eng.profile_enable(True)
+        eng.profile_read(reset=True)
+        eng.exact_lane(pcm_ptr=pcm.data_ptr(), offsets=offs, max_out=10)  # untimed: per-kernel times
+        prof = eng.profile_read(reset=True)
+        eng.profile_enable(False)
+        eng.match_stats(reset=True)
+        k5_ms = sum(prof[k][0] for k in ("match", "vote_hist", "hot_scan", "vote_final") if k in prof)
         top1 = float(np.mean([len(r) > 0 and int(r[0]["track"]) == int(t) for r, t in zip(rows, truth)]))
         same = True
         if ref is None:
@@ -64,7 +79,8 @@ def main():
             same = all(np.array_equal(a, b) for a, b in zip(ref, rows))
         out[name] = {"s": [round(x, 4) for x in ts], "clips_per_s": round(n / min(ts), 1), "top1": top1,
                      "rows_equal_auto": same, "votes_per_query": round(ms["votes"] / max(1, ms["queries"]), 1),
-                     "queries_lds": ms["queries_lds"], "queries_global": ms["queries_global"]}
+                     "queries_lds": ms["queries_lds"], "queries_global": ms["queries_global"],
+                     "k5_ms": round(k5_ms, 3), "k5_frac": round(8 * ms["posting_reads"] / reps_or1(args) / k5_ms / 8e9, 4) if k5_ms else None}
         print(json.dumps({name: out[name]}), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 

@@ -143,10 +143,38 @@ def test_lane_at_44k_odd_windows():
                     for c, t, d, q0, q1 in rows.tolist()]
 
         lane = eng.exact_lane(cs)
+        eng.force("lane_gather", 1)  # the A/B: sub-windows copied to even offsets first
+        try:
+            staged = eng.exact_lane(cs)
+        finally:
+            eng.force("lane_gather", 0)
+        assert all(np.array_equal(a, b) for a, b in zip(lane, staged))
         for i, x in enumerate(cs):
             want = asyncio.run(ex.run_exact_lane(x.astype("<f4").tobytes(), 10, query=query, sample_rate=sr))
             got = ex.candidates_from_rows(lane[i], names, 10)
             assert [(c.track_uuid, c.aligned_hashes, c.offset_seconds, c.confidence) for c in got] == \
                    [(m.track, m.aligned_hashes, m.offset_seconds, m.confidence) for m in want], i
+    finally:
+        eng.close()
+
+
+def test_extract_device_odd_offsets():
+    """Device clips at odd offsets (4-byte aligned float2 frame loads in K1) give the records of the
+    same samples extracted from host copies."""
+    import torch
+
+    sr = 44100
+    eng = Engine(sr, device=0)
+    try:
+        x = np.ascontiguousarray(synth.synth(7, 0, 3 * sr + 5, sr, snr_db=20, salt=3), dtype=np.float32)
+        off = np.array([1, 33075, 66157, 66157 + sr + 2, 3 * sr + 5], np.int64)
+        dev = torch.from_numpy(x).cuda()
+        eng.extract_device(dev.data_ptr(), off)
+        eng.sync()
+        got = [eng.hashes(c) for c in range(len(off) - 1)]
+        want = eng.extract_host([x[off[c]:off[c + 1]] for c in range(len(off) - 1)])
+        for c in range(len(off) - 1):
+            assert len(want[c]) > 0 or off[c + 1] - off[c] < sr // 4
+            assert np.array_equal(got[c], want[c]), c
     finally:
         eng.close()

@@ -92,6 +92,31 @@ def test_level_and_band_robustness(catalog):
         assert len(g) > 0 and g[0, 1] == tr, f"{kind}: true track {tr} not first: {g[:3]}"
         assert abs(g[0, 2] * HOP - start) <= HOP, kind
 
+def test_lds_counter_wrap_long_queries(catalog):
+    """Clean 25 s excerpts give their (track, d) thousands of votes: the LDS path's 8-bit filter counters wrap many
+    times (a wrapped bucket, and each full counter its carry runs through, is marked hot directly). Rows on the LDS
+    path and on the global-histogram path must both equal the oracle's."""
+    eng, tracks = catalog
+    post = eng.index_export()
+    qs = [synth.synth(int(tracks[i]), (i + 1) * 7919, 25 * SR, SR) for i in (1, 5, 9)]
+    qs.append(np.concatenate([qs[0][: 10 * SR], qs[1][: 10 * SR]]))  # two tracks, each far past 255
+    recs = [O.fingerprint(q, HOP) for q in qs]
+    refs = [O.query(post, r, min_match=eng.min_match, max_rows=eng.max_results) for r in recs]
+    assert all(r[0, 0] > 300 for r in refs[:3]) and refs[3][1, 0] > 255
+    try:
+        for path in (1, 2):
+            eng.force("k5_path", path)
+            st0 = eng.match_stats(reset=True)
+            got = eng.query(recs)
+            st = eng.match_stats(reset=True)
+            for q, (g, r) in enumerate(zip(got, refs)):
+                assert np.array_equal(g, r), f"path {path} query {q}"
+            if path == 1:  # answered in LDS, no fallback to the global path
+                assert st["queries_lds"] == len(qs) and st["queries_global"] == 0, (st0, st)
+    finally:
+        eng.force("k5_path", 0)
+
+
 def test_query_extracted_equals_host_query(catalog):
     eng, tracks = catalog
     rng = np.random.default_rng(7)
