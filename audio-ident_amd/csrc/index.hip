@@ -515,7 +515,7 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 //          16-bit counter reaching 0xFFFF, reports nrows = -1 and the host re-runs the query
 //          on the global-histogram path.
 #ifndef AID_K5_LDS_U
-#define AID_K5_LDS_U 4  // A/B builds only
+#define AID_K5_LDS_U 2  // A/B builds only
 #endif
 // 8-bit counters (64 KB) and a 2048-entry exact table: two workgroups per CU, so one query's
 // barriers and table phases overlap another's posting reads. A counter that wraps past 255 marks
