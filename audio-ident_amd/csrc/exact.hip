@@ -12,8 +12,9 @@
 //     by confidence descending, top-N (:118-121).
 // Metadata enrichment (:447-496) stays with the caller (Python, Postgres in the reference).
 //
-// K8a `window_gather` copies each sub-window of the caller's PCM to an even offset of the
-// staging buffer (K1 reads float2 pairs); K8b `exact_consensus` runs one wave per clip over
+// The lane extracts its sub-windows in place (K1's clip table takes overlapping windows); K8a
+// `window_gather`, which copies each sub-window to an even offset of a staging buffer first, is
+// the A/B behind aid_engine_force(LANE_GATHER). K8b `exact_consensus` runs one wave per clip over
 // the K5 rows of its windows (<= 3 x max_results rows, staged in LDS).
 #include "aidfp_device.h"
 
