@@ -338,229 +338,6 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
 #endif
 }
 
-#ifndef AID_K2_SOLO
-#define AID_K2_SOLO 0  // A/B builds only: 1 = one wave per workgroup (k_peak_pick_solo)
-#endif
-#if AID_K2_SOLO
-// K2 with one wave per workgroup: a workgroup is one 256-bin quarter of one strip, and stages its own 64 blocks
-// plus the 4 blocks either side its +-15-bin windows reach (lanes 0..7 load them: 2 x 16 bins of halo per row,
-// zeros past the row's ends). No workgroup barrier (the wave's LDS operations run in order; __syncthreads of a
-// one-wave workgroup compiles to a wave barrier), so no quarter waits for a busier one, and a strip-cold quarter's
-// slot goes to the next workgroup at once. Same decisions, same mask words as k_peak_pick.
-#ifndef AID_K2_SOLO_WPE
-#define AID_K2_SOLO_WPE 0  // A/B: 4 forces 4 waves per SIMD (128 VGPRs, a few spills); 0: 130 VGPRs, 3 waves
-#endif
-__global__ __launch_bounds__(64)
-#if AID_K2_SOLO_WPE
-__attribute__((amdgpu_waves_per_eu(AID_K2_SOLO_WPE)))
-#endif
-void k_peak_pick_solo(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
-                                                       int n_clips, int64_t total_strips, int strip_len, float thr,
-                                                       const uint64_t *__restrict__ hot, uint64_t *__restrict__ mask,
-                                                       uint32_t *__restrict__ cold_cnt) {
-    __shared__ __attribute__((aligned(16))) int rows[kRowsPerStep][256 + 32];  // keys: 16 halo bins each side
-    __shared__ __attribute__((aligned(16))) int bms[kRowsPerStep][64 + 8];     // block maxima: 4 halo blocks each side
-    const int lane = threadIdx.x;
-    constexpr int kInf = 0x7F800000;
-    int64_t unit;
-    {
-        const int64_t nb = gridDim.x, b = blockIdx.x;
-        const int64_t per = nb / 8, rem = nb % 8, x = b % 8, y = b / 8;
-        unit = (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + y;
-        unit = nb - 1 - unit;
-    }
-    const int64_t strip = unit >> 2;
-    const int wave = (int)(unit & 3);  // the quarter
-    if (strip >= total_strips) return;
-    const int tid = wave * 64 + lane;  // block of bins 4 tid .. 4 tid + 3
-    int lo = 0, hi = n_clips - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (clips[mid].strip_base <= strip) lo = mid; else hi = mid - 1;
-    }
-    const int F = (int)clips[lo].frames;
-    const int64_t fb = clips[lo].frame_base;
-    const int t0 = (int)(strip - clips[lo].strip_base) * strip_len;
-    const int t1 = min(t0 + strip_len, F);
-    const float *P = power + fb * kBins;
-    uint64_t *M = mask + fb * kMaskWords + 4 * wave;  // uniform: the lane offset is added at the store (2 VGPRs)
-    const int kthr = __float_as_int(4.0f * thr);
-
-    int m2r[8][4];
-    int pend[8][4];
-    int fprev[4], m7p[4];
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { m2r[s][i] = 0; pend[s][i] = -1; }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { fprev[i] = 0; m7p[i] = 0; }
-    const uint64_t b0ok = __ballot(tid != 0);
-
-    const int rbeg = t0 - kPeakDT;
-    const int iters = (t1 - t0) + 2 * kPeakDT;
-    const uint64_t *HW = hot + fb;
-    const int myb = hot_bit(tid >> 2);
-    // halo bin of lanes 0..31 (one dword each): bins 256 q - 16 .. 256 q - 1 and 256 q + 256 .. 256 q + 271
-    const int hbin = lane < 16 ? 256 * wave - 16 + lane : 256 * wave + 240 + lane;
-    const bool hvalid = lane < 32 && hbin >= 0 && hbin < kBins;
-    const uint32_t hbyte = hvalid ? 4u * (uint32_t)hbin : 0x80000000u;  // byte offset in a row, or none
-    const int hbit = hvalid ? hot_bit(hbin >> 4) : 0;
-    auto hotword = [&](int r) -> uint64_t { return (r >= 0 && r < F) ? HW[r] : 0ull; };
-    auto hotwords = [&](int rb) -> uint64_t {
-        const int r = rb + (lane & 3);
-        return (r >= 0 && r < F) ? HW[r] : 0ull;
-    };
-    auto word_of = [](uint64_t v, int j) -> uint64_t {
-        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), j) << 32) |
-               (uint32_t)__builtin_amdgcn_readlane((int)v, j);
-    };
-    uint64_t wmask = 0;
-    for (int c = max(16 * wave - 1, 0); c <= min(16 * wave + 16, 63); ++c) wmask |= 1ull << hot_bit(c);
-    {
-        uint64_t acc = 0;
-        for (int r = rbeg + lane; r < rbeg + iters; r += 64) acc |= (r >= 0 && r < F) ? HW[r] : 0ull;
-        if (__ballot((acc & wmask) != 0ull) == 0) {  // strip-cold quarter: zero mask words, done
-            uint64_t *Mz = mask + fb * kMaskWords + 4 * wave + (lane & 3);
-            for (int r = t0 + (lane >> 2); r < t1; r += 16) Mz[(int64_t)r * kMaskWords] = 0;
-            if (lane == 0 && cold_cnt) atomicAdd(&cold_cnt[blockIdx.x & 63], 1u);
-            return;
-        }
-    }
-    const int rlo = max(rbeg, 0), rhi = min(rbeg + iters, F);
-    const __amdgpu_buffer_rsrc_t rows_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(P + (int64_t)rlo * kBins), (short)0, (rhi - rlo) * kBins * 4, 0x00020000);
-    constexpr uint32_t kOOB = 0x80000000u;
-    auto load_row = [&](int r, uint64_t hwr) -> float4 {
-        const uint32_t off = ((hwr >> myb) & 1ull) ? (uint32_t)(r - rlo) * (kBins * 4) + 16u * tid : kOOB;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rows_rsrc, off, 0, 0);
-        return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
-    };
-    auto load_halo = [&](int r, uint64_t hwr) -> float {
-        const uint32_t off = hbyte != kOOB && ((hwr >> hbit) & 1ull) ? (uint32_t)(r - rlo) * (kBins * 4) + hbyte : kOOB;
-        return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rows_rsrc, off, 0, 0));
-    };
-    float4 pf[kRowsPerStep];
-    float ph[kRowsPerStep];
-#pragma unroll
-    for (int j = 0; j < kRowsPerStep; ++j) {
-        const uint64_t w = j < iters ? hotword(rbeg + j) : 0ull;
-        pf[j] = load_row(rbeg + j, w);
-        ph[j] = load_halo(rbeg + j, w);
-    }
-    uint64_t hwv = hotwords(rbeg + kRowsPerStep);
-    uint64_t hsave[kRowsPerStep], hcur[kRowsPerStep];
-#pragma unroll
-    for (int j = 0; j < kRowsPerStep; ++j) hsave[j] = hcur[j] = hotword(rbeg + j);
-
-    for (int base = 0; base < iters; base += 8) {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int it = base + s;
-            if (it >= iters) break;
-            if (s % kRowsPerStep == 0) {
-#pragma unroll
-                for (int j = 0; j < kRowsPerStep; ++j) {
-                    const int slot = (s + j) % kRowsPerStep;
-                    const float4 v = pf[slot];
-                    const int4 kv = make_int4(pkey(v.x), pkey(v.y), pkey(v.z), pkey(v.w));
-                    reinterpret_cast<int4 *>(&rows[j][16])[lane] = kv;
-                    bms[j][4 + lane] = max(max(kv.x, kv.y), max(kv.z, kv.w));
-                    {
-                        const int ku = pkey(ph[slot]);
-                        // the halo blocks' maxima: a max over each lane quad (DPP quad permutes)
-                        int km = max(ku, __builtin_amdgcn_update_dpp(0, ku, 0xB1, 0xF, 0xF, false));  // quad [1,0,3,2]
-                        km = max(km, __builtin_amdgcn_update_dpp(0, km, 0x4E, 0xF, 0xF, false));     // quad [2,3,0,1]
-                        if (lane < 32) {
-                            const int hslot = lane < 16 ? lane : 256 + lane;  // key slot (halo block: slot / 4)
-                            rows[j][hslot] = ku;
-                            if ((lane & 3) == 0) bms[j][hslot >> 2] = km;
-                        }
-                    }
-                    const int rn = rbeg + it + j + kRowsPerStep;
-                    hcur[j] = hsave[j];
-                    hsave[j] = word_of(hwv, j);
-                    const uint64_t w = it + j + kRowsPerStep < iters ? hsave[j] : 0ull;
-                    pf[slot] = load_row(rn, w);
-                    ph[slot] = load_halo(rn, w);
-                }
-                hwv = hotwords(rbeg + it + 2 * kRowsPerStep);
-                __syncthreads();  // one wave: a wave barrier (orders the cross-lane LDS reads after the writes)
-            }
-            const int r = rbeg + it;
-            bool pk[4];
-            uint64_t bal[4];
-            if (!(hcur[s % kRowsPerStep] & wmask)) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int m2 = fprev[i];
-                    fprev[i] = 0;
-                    m2r[s][i] = m2;
-                    const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
-                    m7p[i] = m7;
-                    pk[i] = pend[(s + 1) & 7][i] >= m7;
-                    bal[i] = __ballot(pk[i]);
-                    pend[s][i] = -1;
-                }
-            } else {
-            const int4 *rb4 = reinterpret_cast<const int4 *>(rows[s % kRowsPerStep]);
-            const int *bm = bms[s % kRowsPerStep];
-            const int4 lf = rb4[lane], me = rb4[lane + 4], rt = rb4[lane + 8];
-            asm volatile("" ::"v"(lf.x), "v"(rt.w));
-            const int M3L = max(max(bm[lane + 1], bm[lane + 2]), bm[lane + 3]);
-            const int M3R = max(max(bm[lane + 5], bm[lane + 6]), bm[lane + 7]);
-            const int lsuf2 = max(lf.z, lf.w), lsuf1 = max(lf.y, lsuf2);
-            const int rpre1 = max(rt.x, rt.y), rpre2 = max(rpre1, rt.z);
-            const int mpre1 = max(me.x, me.y), mpre2 = max(mpre1, me.z);
-            const int msuf2 = max(me.z, me.w), msuf1 = max(me.y, msuf2);
-            int L[4], R[4];
-            L[0] = max(lsuf1, M3L);
-            L[1] = max(max(lsuf2, M3L), me.x);
-            L[2] = max(max(lf.w, M3L), mpre1);
-            L[3] = max(M3L, mpre2);
-            R[0] = max(msuf1, M3R);
-            R[1] = max(max(msuf2, M3R), rt.x);
-            R[2] = max(max(me.w, M3R), rpre1);
-            R[3] = max(M3R, rpre2);
-            const int mev[4] = {me.x, me.y, me.z, me.w};
-            const int thr_row = (r >= t0 && r < t1) ? kthr : kInf;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int p = mev[i];
-                const int fm = max(max(L[i], p), R[i]);
-                const int m2 = max(fm, fprev[i]);
-                fprev[i] = fm;
-                const int bf = max(max(L[i], thr_row), m7p[i]);
-                m2r[s][i] = m2;
-                const int m7 = max(max(max(m2, m2r[(s - 2) & 7][i]), m2r[(s - 4) & 7][i]), m2r[(s - 5) & 7][i]);
-                m7p[i] = m7;
-                pk[i] = pend[(s + 1) & 7][i] >= m7;
-                bal[i] = __ballot(pk[i]);
-                bool cand = p > bf && p >= R[i];
-                if (i == 0) cand = cand && ((b0ok >> lane) & 1ull);
-                pend[s][i] = cand ? p : -1;
-            }
-            }
-            const uint64_t b0 = bal[0], b1 = bal[1], b2 = bal[2], b3 = bal[3];
-            const int rd = r - kPeakDT;
-            if (rd >= t0 && rd < t1) {
-                uint32_t lo32, hi32;
-                asm volatile("" : "=v"(lo32), "=v"(hi32));
-                lo32 = write_lane<0>(lo32, (uint32_t)b0);
-                hi32 = write_lane<0>(hi32, (uint32_t)(b0 >> 32));
-                lo32 = write_lane<1>(lo32, (uint32_t)b1);
-                hi32 = write_lane<1>(hi32, (uint32_t)(b1 >> 32));
-                lo32 = write_lane<2>(lo32, (uint32_t)b2);
-                hi32 = write_lane<2>(hi32, (uint32_t)(b2 >> 32));
-                lo32 = write_lane<3>(lo32, (uint32_t)b3);
-                hi32 = write_lane<3>(hi32, (uint32_t)(b3 >> 32));
-                if (lane < 4) M[(int64_t)rd * kMaskWords + lane] = ((uint64_t)hi32 << 32) | lo32;
-            }
-        }
-    }
-}
-#endif
-
 #if defined(AID_K2_STAMPS)
 int k2_stamps_read(unsigned long long *out, bool reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_k2_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -2;
@@ -575,25 +352,15 @@ int k2_stamps_read(unsigned long long *out, bool reset) {
 void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
                       float thr, const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {
     if (total_strips <= 0) return;
-#if AID_K2_SOLO
-    timed_launch(k_peak_pick_solo, dim3((unsigned)(4 * total_strips)), dim3(64), 0, s, power, clips, n_clips,
-                 total_strips, strip_len, thr, hot, mask, cold_cnt);
-#else
     timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
                  strip_len, thr, hot, mask, cold_cnt);
-#endif
 }
 
-// resident K2 strips per CU (registers / LDS), for sizing strips to one round
+// resident K2 workgroups per CU (registers / LDS), for sizing strips to one round
 int peak_pick_blocks_per_cu() {
     int n = 0;
-#if AID_K2_SOLO
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_peak_pick_solo, 64, 0) != hipSuccess || n < 4) n = 4;
-    return n / 4;  // four quarter workgroups per strip
-#else
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_peak_pick, 256, 0) != hipSuccess || n <= 0) n = 1;
     return n;
-#endif
 }
 
 }  // namespace aid
