@@ -324,8 +324,9 @@ class Engine:
         check(self._lib.aid_index_load(self._h, str(path).encode()))
 
     def _rows(self, rows, nrows, nq: int) -> list[np.ndarray]:
-        arr = np.ctypeslib.as_array(rows).view(np.int32).reshape(nq, self.max_results, 5)
-        return [arr[q, : nrows[q]].astype(np.int64) for q in range(nq)]
+        # one conversion for the batch, then per-query views (a per-query astype cost ~1 us each)
+        arr = np.ctypeslib.as_array(rows).view(np.int32).reshape(nq, self.max_results, 5).astype(np.int64)
+        return [r[:k] for r, k in zip(arr, nrows.tolist())]
 
     def query(self, queries) -> list[np.ndarray]:
         """Match host record arrays; per query [r, 5] int64 rows (count, track, d, tq_min, tq_max)."""
@@ -395,7 +396,8 @@ class Engine:
         out = np.zeros(n * max_out, dtype=self.EXACT_DTYPE)
         nout = np.zeros(n, dtype=np.int32)
         check(self._lib.aid_exact_lane(self._h, src, _p(offsets), n, loc, max_out, _p(out), _p(nout), None))
-        return [out[c * max_out: c * max_out + nout[c]].copy() for c in range(n)]
+        # per-clip views of the one result array (4096 per-clip copies took ~3.5 ms of host time per lane call)
+        return [r[:k] for r, k in zip(out.reshape(n, max_out), nout.tolist())]
 
     def downmix(self, stereo_ptr: int, n_frames: int, mono_ptr: int, stream: int | None = None) -> None:
         check(self._lib.aid_downmix(self._h, ctypes.c_void_p(stereo_ptr), int(n_frames), ctypes.c_void_p(mono_ptr),
