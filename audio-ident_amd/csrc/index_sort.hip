@@ -40,7 +40,10 @@ constexpr int kSortKeyBits = 27;  // key26 plus the removed-posting sentinel 2^2
 constexpr int kDigitBits = 9;
 constexpr int kDigits = 1 << kDigitBits;
 constexpr int kSortPasses = 3;
-constexpr int kSortThreads = 256;  // 4 waves
+#ifndef AID_K4_THREADS
+#define AID_K4_THREADS 256  // A/B builds only
+#endif
+constexpr int kSortThreads = AID_K4_THREADS;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
 #ifndef AID_K4_SLOTS
 #define AID_K4_SLOTS 16  // A/B builds only (build_ext variant defines)
