@@ -35,6 +35,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -614,6 +615,9 @@ def main() -> int:
                     help="seconds of untimed steps after the warmup steps (GPU clock ramp); 0 = none")
     ap.add_argument("--no-fullband", action="store_true", help="skip the full-band workload key")
     ap.add_argument("--no-catalog", action="store_true", help="skip the config-3 catalog leg")
+    ap.add_argument("--leg-deadline", type=float, default=float(os.environ.get("AIDFP_BENCH_LEG_DEADLINE", 300)),
+                    help="seconds after the headline within which the extra legs must finish; past it the line is "
+                         "printed without them and the process ends (0 = no deadline)")
     ap.add_argument("--catalog-tracks", type=int, default=100000)
     ap.add_argument("--catalog-seconds", type=float, default=30.0)
     ap.add_argument("--exact-clips", type=int, default=10000,
@@ -778,24 +782,40 @@ def main() -> int:
     torch.cuda.empty_cache()
 
     _log("fullband done")
-    catalog = None
-    if not args.no_catalog:
-        try:
-            catalog = catalog_leg(args, rank, world, dist, torch)
-        except Exception as exc:  # the headline stands on its own
-            catalog = {"error": f"{type(exc).__name__}: {exc}"}
+    # The extra legs (catalog ingest with its RCCL exchange, exact lane, service) run after the headline is measured.
+    # A leg that never returns (a collective stuck on some rank) must not cost the headline line: past the deadline a
+    # watchdog prints the line with the unfinished legs marked and ends the process (every rank runs the same timer)
+    legs = {"catalog": None, "service": None}
+    emitted = threading.Lock()
+    finished = threading.Event()
 
-    _log("catalog + exact lane done")
-    service = None
-    if not args.no_service:
-        try:  # service_leg agrees on its rank-local parts, so every rank takes this branch alike
-            service = service_leg(args, rank, world, dist, torch)
-        except Exception as exc:  # the headline stands on its own
-            service = {"error": f"{type(exc).__name__}: {exc}"}
+    def emit_line() -> bool:
+        if not emitted.acquire(blocking=False):
+            return False
+        if rank == 0:
+            print(json.dumps(make_line(legs["catalog"], legs["service"])), flush=True)
+        return True
 
-    _log("service done")
-    if rank == 0:
-        line = {
+    def watchdog():
+        if finished.wait(args.leg_deadline):
+            return
+        for k in legs:
+            if legs[k] is None and not getattr(args, f"no_{k}"):
+                legs[k] = {"error": f"deadline: not finished {args.leg_deadline:.0f} s after the headline"}
+        _log("leg deadline passed: printing the line without the unfinished legs and exiting")
+        if emit_line():
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0 if ok_headline() else 1)
+
+    def ok_headline() -> bool:
+        ok = par is None or par["bit_exact"]
+        if fullband and "parity" in fullband:
+            ok = ok and fullband["parity"]["bit_exact"]
+        return ok
+
+    def make_line(catalog, service) -> dict:
+        return {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "audio-s/s",
@@ -829,13 +849,33 @@ def main() -> int:
             "cpu_baseline": cpu,
             "parity": par,
         }
-        print(json.dumps(line), flush=True)
+
+    if args.leg_deadline > 0 and not (args.no_catalog and args.no_service):
+        threading.Thread(target=watchdog, daemon=True).start()
+    catalog = None
+    if not args.no_catalog:
+        try:
+            catalog = catalog_leg(args, rank, world, dist, torch)
+        except Exception as exc:  # the headline stands on its own
+            catalog = {"error": f"{type(exc).__name__}: {exc}"}
+        legs["catalog"] = catalog
+
+    _log("catalog + exact lane done")
+    service = None
+    if not args.no_service:
+        try:  # service_leg agrees on its rank-local parts, so every rank takes this branch alike
+            service = service_leg(args, rank, world, dist, torch)
+        except Exception as exc:  # the headline stands on its own
+            service = {"error": f"{type(exc).__name__}: {exc}"}
+        legs["service"] = service
+
+    _log("service done")
+    finished.set()
+    if not emit_line():  # the watchdog printed the line and is ending the process
+        threading.Event().wait()
     if dist:
         dist.destroy_process_group()
-    ok = par is None or par["bit_exact"]
-    if fullband and "parity" in fullband:
-        ok = ok and fullband["parity"]["bit_exact"]
-    return 0 if ok else 1
+    return 0 if ok_headline() else 1
 
 
 if __name__ == "__main__":
