@@ -8,6 +8,7 @@ only); nothing here computes a fingerprint itself.
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Sequence
 
 import numpy as np
@@ -22,6 +23,33 @@ BINS = 1024
 
 def _p(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
+
+
+_pinned = threading.local()
+_PINNED_MAX = 16 << 20  # floats (64 MiB: the query coalescer's batch cap); larger host batches stay pageable
+
+
+def _host_concat(arrs: list[np.ndarray], total: int) -> np.ndarray:
+    """The clips concatenated into one host array for AID_PCM_HOST. Up to _PINNED_MAX samples it is a page-locked
+    buffer of the calling thread (grown on demand), so the engine's single H2D copy of the span runs as a DMA
+    instead of through the runtime's pageable staging (coalesced service queries); the engine call has finished
+    with it when it returns (every host-PCM entry point syncs before returning its results)."""
+    if total == 0:
+        return np.zeros(1, dtype=np.float32)
+    if total <= _PINNED_MAX:
+        try:
+            import torch
+
+            buf = getattr(_pinned, "buf", None)
+            if buf is None or buf.numel() < total:
+                buf = torch.empty(max(total, 1 << 20), dtype=torch.float32, pin_memory=True)
+                _pinned.buf = buf
+            out = buf.numpy()[:total]
+            np.concatenate(arrs, out=out)
+            return out
+        except (ImportError, RuntimeError):  # no torch / no device: pageable memory works the same, slower
+            pass
+    return np.concatenate(arrs)
 
 
 class Engine:
@@ -98,9 +126,7 @@ class Engine:
         offsets = np.zeros(len(arrs) + 1, dtype=np.int64)
         if arrs:
             offsets[1:] = np.cumsum([len(a) for a in arrs])
-        pcm = np.concatenate(arrs) if arrs else np.zeros(1, dtype=np.float32)
-        if pcm.size == 0:
-            pcm = np.zeros(1, dtype=np.float32)
+        pcm = _host_concat(arrs, int(offsets[-1]))
         check(self._lib.aid_extract(self._h, _p(pcm), _p(offsets), len(arrs), AID_PCM_HOST, None))
         self.n_clips = len(arrs)
         return [self.hashes(c) for c in range(len(arrs))]
@@ -360,7 +386,7 @@ class Engine:
             return []
         offsets = np.zeros(nq + 1, dtype=np.int64)
         offsets[1:] = np.cumsum([len(a) for a in arrs])
-        pcm = np.concatenate(arrs) if offsets[-1] else np.zeros(1, dtype=np.float32)
+        pcm = _host_concat(arrs, int(offsets[-1]))
         rows = (AidMatchRow * (nq * self.max_results))()
         nrows = np.zeros(nq, dtype=np.int32)
         check(self._lib.aid_query_pcm(self._h, _p(pcm), _p(offsets), nq, AID_PCM_HOST, ctypes.addressof(rows),
@@ -385,7 +411,7 @@ class Engine:
             offsets = np.zeros(len(arrs) + 1, dtype=np.int64)
             if arrs:
                 offsets[1:] = np.cumsum([len(a) for a in arrs])
-            pcm = np.concatenate(arrs) if arrs and offsets[-1] else np.zeros(1, dtype=np.float32)
+            pcm = _host_concat(arrs, int(offsets[-1]))
             src, loc = _p(pcm), AID_PCM_HOST
         else:
             offsets = np.ascontiguousarray(offsets, dtype=np.int64)
