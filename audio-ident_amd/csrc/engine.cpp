@@ -69,7 +69,8 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
-                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s);
+                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, const int64_t *votes,
+                      hipStream_t s);
 uint32_t index_keys();
 void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
 void launch_window_gather(const float *src, const int64_t *win, int n_win, int64_t max_len, float *dst, hipStream_t s);
@@ -1837,7 +1838,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         {
             ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, s);
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p, s);
         }
         HIP_TRY(hipGetLastError());
         spec_n.resize(nq);
@@ -1895,7 +1896,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         {
             ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, s);
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p, s);
         }
         HIP_TRY(hipGetLastError());
         std::vector<int32_t> got_n(nq);

@@ -198,6 +198,7 @@ struct QueryParams {
     int32_t tomb_live;         // 0: the CSR holds no posting of a removed track (skip tomb[] loads)
     uint32_t *hot;             // [nq][2^hist_bits / 32] bit per histogram bucket >= min_match (K5h)
     int32_t parts;             // K5a workgroups (key partitions) per query
+    const int64_t *votes;      // [nq] exact votes per query (k_query_votes, earlier on the stream); LDS path only
 };
 
 // Every vote (track, d = t_ref - t_q, t_q) of query records [a, a + n), for the calling wave's
@@ -549,7 +550,6 @@ struct FastLds {
     } u;
     uint32_t hot[(1 << kLdsHistBits) / 32];
     int32_t out_n, overflow;
-    uint32_t votes;
 };
 
 __global__ __launch_bounds__(kFastThreads)
@@ -566,21 +566,11 @@ void k_match_lds(QueryParams qp) {
     for (int i = tid; i < (1 << kLdsHistBits) / kLdsCtrPerWord; i += kFastThreads) L.u.hist[i] = 0u;
     if (AID_K5_LDS8)
         for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
-    if (tid == 0) { L.out_n = 0; L.overflow = 0; L.votes = 0; }
+    if (tid == 0) { L.out_n = 0; L.overflow = 0; }
     __syncthreads();
-    // total votes (sum of the records' bucket lengths): below the counter maximum no counter can
-    // wrap, so only heavier queries pay for returning atomics (the carry check below)
-    {
-        uint32_t v = 0;
-        for (int64_t i = tid; i < n; i += kFastThreads) {
-            const uint32_t k = key26((uint32_t)qp.recs[a + i]);
-            v += qp.offsets[k + 1] - qp.offsets[k];
-        }
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) atomicAdd(&L.votes, v);
-    }
-    __syncthreads();
-    const bool check_wrap = L.votes >= kLdsCtrMax;
+    // the query's exact vote total (k_query_votes): below the counter maximum no counter can wrap, so only
+    // heavier queries pay for returning atomics (the carry check below)
+    const bool check_wrap = qp.votes[q] >= (int64_t)kLdsCtrMax;
     // phase 1
     for_each_vote<kLdsWindows>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
         const uint32_t h = mix_td(tr, d) & hmask;
@@ -718,10 +708,11 @@ void k_match_lds(QueryParams qp) {
 
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
-                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, hipStream_t s) {
+                      int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, const int64_t *votes,
+                      hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
-                   tomb_live, nullptr, 1};
+                   tomb_live, nullptr, 1, votes};
     timed_launch(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
 }
 
@@ -758,7 +749,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
                   int parts, int stage, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
-                   nrows, tomb_live, hot, parts};
+                   nrows, tomb_live, hot, parts, nullptr};
     // stage = 0: all three kernels; 1, 2, 3: K5a, K5h, K5b alone (the engine times them one by one)
     if (stage == 0 || stage == 1) timed_launch(k_vote_hist, dim3(nq * parts), dim3(1024), 0, s, qp);
     if (stage == 0 || stage == 2)
