@@ -557,7 +557,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     hipStream_t s = pick_stream(e, stream);
     const int hop = e->cfg.hop;
 
-    // descriptors; host PCM is re-packed at even offsets
+    // descriptors; host PCM is staged as one copy of the clips' span
     if ((size_t)n_clips + 1 > e->h_desc_cap) {
         if (e->h_desc) HIP_TRY(hipHostFree(e->h_desc));
         e->h_desc = nullptr;
