@@ -530,12 +530,21 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 #define AID_K5_LDS_THREADS 1024
 #endif
 constexpr int kLdsWindows = AID_K5_LDS_U;  // windows of 64 posting loads a wave keeps in flight (LDS path)
-constexpr int kLdsHistBits = 16;
+#ifndef AID_K5_HBITS
+#define AID_K5_HBITS 16  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
+#endif
+constexpr int kLdsHistBits = AID_K5_HBITS;
 constexpr int kLdsCtrBits = AID_K5_LDS8 ? 8 : 16;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
-constexpr int kFastVoteCap = AID_K5_LDS8 ? 2048 : 4096;
-constexpr int kFastTrackCap = 1024;
+#ifndef AID_K5_VCAP
+#define AID_K5_VCAP (AID_K5_LDS8 ? 2048 : 4096)
+#endif
+constexpr int kFastVoteCap = AID_K5_VCAP;
+#ifndef AID_K5_TCAP
+#define AID_K5_TCAP 1024
+#endif
+constexpr int kFastTrackCap = AID_K5_TCAP;
 constexpr int kFastThreads = AID_K5_LDS_THREADS;
 
 struct FastLds {
@@ -554,7 +563,10 @@ struct FastLds {
 
 __global__ __launch_bounds__(kFastThreads)
 #if AID_K5_LDS8
-__attribute__((amdgpu_waves_per_eu(2 * kFastThreads / 256)))
+#ifndef AID_K5_WPE
+#define AID_K5_WPE (2 * AID_K5_LDS_THREADS / 256)
+#endif
+__attribute__((amdgpu_waves_per_eu(AID_K5_WPE)))
 #endif
 void k_match_lds(QueryParams qp) {
     __shared__ FastLds L;  // 8-bit counters: 72 KB, two workgroups per CU (16-bit: 136 KB, one)
