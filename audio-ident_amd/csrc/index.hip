@@ -518,9 +518,9 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 #ifndef AID_K5_LDS_U
 #define AID_K5_LDS_U 2  // A/B builds only
 #endif
-// 8-bit counters (2^15 of them, 32 KB) and a 1024-entry exact table (36 KB in all): four 512-thread workgroups
-// per CU, so one query's barriers and table phases overlap the others' posting reads (two 1024-thread workgroups
-// with 2^16 counters: K5 +2.5 %, profiles/r04zp_k5_four_workgroups_ab.txt). A counter that wraps past 255 marks
+// 8-bit counters (64 KB) and a 2048-entry exact table: two workgroups per CU, so one query's
+// barriers and table phases overlap another's posting reads. (Four 512-thread workgroups with 2^15 counters and a
+// 1024-entry table ran K5 2.5 % faster on config 4 but sent a bench query to the global path: dropped.) A counter that wraps past 255 marks
 // its bucket hot at once (>= 256 votes), as does any full counter its carry runs through, so the
 // filter stays an exact superset; with 16-bit counters (one workgroup per CU) a wrap hands the
 // query to the global path.
@@ -528,22 +528,22 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 #define AID_K5_LDS8 1  // A/B builds only: 0 = 16-bit counters
 #endif
 #ifndef AID_K5_LDS_THREADS
-#define AID_K5_LDS_THREADS 512
+#define AID_K5_LDS_THREADS 1024
 #endif
 constexpr int kLdsWindows = AID_K5_LDS_U;  // windows of 64 posting loads a wave keeps in flight (LDS path)
 #ifndef AID_K5_HBITS
-#define AID_K5_HBITS 15  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
+#define AID_K5_HBITS 16  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
 #endif
 constexpr int kLdsHistBits = AID_K5_HBITS;
 constexpr int kLdsCtrBits = AID_K5_LDS8 ? 8 : 16;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
 #ifndef AID_K5_VCAP
-#define AID_K5_VCAP (AID_K5_LDS8 ? 1024 : 4096)
+#define AID_K5_VCAP (AID_K5_LDS8 ? 2048 : 4096)
 #endif
 constexpr int kFastVoteCap = AID_K5_VCAP;
 #ifndef AID_K5_TCAP
-#define AID_K5_TCAP 512
+#define AID_K5_TCAP 1024
 #endif
 constexpr int kFastTrackCap = AID_K5_TCAP;
 constexpr int kFastThreads = AID_K5_LDS_THREADS;
@@ -565,7 +565,7 @@ struct FastLds {
 __global__ __launch_bounds__(kFastThreads)
 #if AID_K5_LDS8
 #ifndef AID_K5_WPE
-#define AID_K5_WPE 8
+#define AID_K5_WPE (2 * AID_K5_LDS_THREADS / 256)
 #endif
 __attribute__((amdgpu_waves_per_eu(AID_K5_WPE)))
 #endif
