@@ -7,8 +7,11 @@ only); nothing here computes a fingerprint itself.
 
 from __future__ import annotations
 
+import atexit
 import ctypes
+import sys
 import threading
+import weakref
 from typing import Sequence
 
 import numpy as np
@@ -25,8 +28,80 @@ def _p(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
+class _PinnedSlot:
+    """One thread's page-locked staging buffer (a thread's slot dies with the thread)."""
+
+    __slots__ = ("buf", "__weakref__")
+
+    def __init__(self):
+        self.buf = None
+
+
 _pinned = threading.local()
 _PINNED_MAX = 16 << 20  # floats (64 MiB: the query coalescer's batch cap); larger host batches stay pageable
+
+# Ordered teardown. Everything that owns device or page-locked memory is released from ONE atexit hook, registered
+# after torch's own (atexit runs last-registered first), so it runs while the HIP runtime, torch's allocators and
+# any profiler tool (rocprofv3) are all still alive: the live engines are destroyed, the service threads joined,
+# every thread's page-locked staging buffer dropped and torch's pinned cache emptied. Afterwards Engine.__del__ is
+# a no-op, so nothing calls into HIP while the interpreter or the C runtime tears down.
+_live: "weakref.WeakSet[Engine]" = weakref.WeakSet()
+_pinned_slots: "weakref.WeakSet[_PinnedSlot]" = weakref.WeakSet()  # every live thread's staging slot
+_closers: "weakref.WeakSet" = weakref.WeakSet()  # objects closed first (FingerprintService: its threads, its engine)
+_shutdown_done = False
+_hook_lock = threading.Lock()
+_hook_registered = False
+
+
+def _finalizing() -> bool:
+    return _shutdown_done or sys.is_finalizing()
+
+
+def on_shutdown(obj) -> None:
+    """obj.close() runs in the ordered teardown before the engines are destroyed (a service joins its threads
+    first). Held weakly: an object that is gone by then has nothing left to close."""
+    _register_hook()
+    _closers.add(obj)
+
+
+def _shutdown() -> None:
+    global _shutdown_done
+    if _shutdown_done:
+        return
+    for obj in list(_closers):
+        try:
+            obj.close()
+        except Exception:  # teardown goes on: every engine must still be destroyed
+            pass
+    for e in list(_live):
+        try:
+            e.close()
+        except Exception:
+            pass
+    for sl in list(_pinned_slots):
+        sl.buf = None
+    try:
+        import torch
+
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+            torch._C._host_emptyCache()  # page-locked blocks back to the runtime while it is alive
+    except Exception:
+        pass
+    _shutdown_done = True
+
+
+def _register_hook() -> None:
+    global _hook_registered
+    with _hook_lock:
+        if _hook_registered:
+            return
+        try:  # torch registers its atexit handlers at import: import it first, so this hook runs before them
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        atexit.register(_shutdown)
+        _hook_registered = True
 
 
 def _host_concat(arrs: list[np.ndarray], total: int) -> np.ndarray:
@@ -40,10 +115,15 @@ def _host_concat(arrs: list[np.ndarray], total: int) -> np.ndarray:
         try:
             import torch
 
-            buf = getattr(_pinned, "buf", None)
+            sl = getattr(_pinned, "slot", None)
+            if sl is None:
+                sl = _pinned.slot = _PinnedSlot()
+                _pinned_slots.add(sl)
+            buf = sl.buf
             if buf is None or buf.numel() < total:
-                buf = torch.empty(max(total, 1 << 20), dtype=torch.float32, pin_memory=True)
-                _pinned.buf = buf
+                if _finalizing():
+                    raise RuntimeError("interpreter shutting down")
+                buf = sl.buf = torch.empty(max(total, 1 << 20), dtype=torch.float32, pin_memory=True)
             out = buf.numpy()[:total]
             np.concatenate(arrs, out=out)
             return out
@@ -69,6 +149,7 @@ class Engine:
             cfg.max_results = max_results
         if keep_power:  # parity/debug: the whole power plane for power() (K1 otherwise skips cold blocks)
             cfg.flags |= L.AID_FLAG_KEEP_POWER
+        _register_hook()
         h = ctypes.c_void_p()
         rc = lib.aid_engine_create(ctypes.byref(cfg), ctypes.byref(h))
         if rc == AID_ERR_DEVICE:
@@ -85,6 +166,7 @@ class Engine:
         self.min_match = out.min_match
         self.max_results = out.max_results
         self.n_clips = 0
+        _live.add(self)
 
     # -- lifecycle --
     def close(self) -> None:
@@ -93,6 +175,8 @@ class Engine:
             self._h = None
 
     def __del__(self):  # pragma: no cover
+        if _finalizing():  # the ordered teardown (_shutdown) already destroyed every live engine
+            return
         try:
             self.close()
         except Exception:

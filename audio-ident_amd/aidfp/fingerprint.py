@@ -124,6 +124,9 @@ class FingerprintService:
         # ingest); the catalog on disk is still loaded first, and checkpoint() writes everything
         self.persist = True
         self.checkpoint_min_bytes = checkpoint_min_bytes
+        from .engine import on_shutdown
+
+        on_shutdown(self)  # closed (coalescer thread joined, engine destroyed) at exit, before the HIP runtime goes
 
     # -- engine and persistence --
     def _eng(self):
@@ -276,17 +279,20 @@ class FingerprintService:
         return self._coalescer(pcm)
 
     def _query_rows(self, eng, pcms: list[bytes]) -> list:
-        """Engine rows per request. If the batch's engine call fails (one request's vote table overflows, a
-        large batch runs out of device memory), the batch is bisected and retried, so only the request that
-        fails on its own gets [] -- like one failing `olaf_c query` process (fingerprint.py:197-200)."""
-        from ._lib import EngineError
+        """Engine rows per request. If the batch's engine call fails in a way that depends on the batch (one
+        request's vote table overflows: AID_ERR_STATE; a large batch runs out of memory: AID_ERR_NOMEM), the
+        batch is bisected and retried, so only the request that fails on its own gets [] -- like one failing
+        `olaf_c query` process (fingerprint.py:197-200). A device fault or an invalid argument does not depend
+        on the batch: the whole batch gets [] at once (bisecting a sticky device fault would cost ~2n failing
+        engine calls under the shared lock)."""
+        from ._lib import AID_ERR_NOMEM, AID_ERR_STATE, EngineError
 
         try:
             return eng.query_pcm([self._pcm(p) for p in pcms])
         except EngineError as exc:
-            if len(pcms) == 1:
-                logger.error("aidfp query failed: %s", exc)
-                return [np.zeros((0, 5), np.int64)]
+            if len(pcms) == 1 or exc.code not in (AID_ERR_STATE, AID_ERR_NOMEM):
+                logger.error("aidfp query batch of %d failed: %s", len(pcms), exc)
+                return [np.zeros((0, 5), np.int64) for _ in pcms]
             logger.warning("aidfp query batch of %d failed (%s); retrying in halves", len(pcms), exc)
         h = len(pcms) // 2
         return self._query_rows(eng, pcms[:h]) + self._query_rows(eng, pcms[h:])

@@ -311,6 +311,15 @@ static hipStream_t pick_stream(aid_engine *e, void *stream) {
     return stream ? (hipStream_t)stream : e->own_stream;
 }
 
+// A host-PCM call copies the caller's samples with ONE hipMemcpyAsync on the call's stream; from page-locked
+// memory that copy is a real DMA that can still be running when the call returns. On success the caller syncs
+// before reusing its buffer (include/aidfp.h); on an error return the engine drains the stream itself, so a
+// caller that reuses or frees its buffer after a failed call cannot race the copy. Returns rc.
+static int drain_host_copy(aid_engine *e, int32_t loc, void *stream, int rc) {
+    if (rc != AID_OK && loc == AID_PCM_HOST && e) (void)hipStreamSynchronize(pick_stream(e, stream));
+    return rc;
+}
+
 extern "C" {
 
 int32_t aid_abi_version(void) { return AID_ABI_VERSION; }
@@ -544,7 +553,7 @@ int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t
         if (offsets[c + 1] < offsets[c] || offsets[c] < 0)
             return fail(AID_ERR_INVALID, "aid_extract: offsets must be non-decreasing and >= 0");
     std::lock_guard<std::mutex> lk(e->mu);
-    return extract_locked(e, pcm, offsets, n_clips, loc, stream);
+    return drain_host_copy(e, loc, stream, extract_locked(e, pcm, offsets, n_clips, loc, stream));
 }
 
 // Clip c is pcm[offsets[c], offsets[c + 1]); with `ends` (device PCM only) it is pcm[offsets[c], ends[c]), so
@@ -2045,8 +2054,8 @@ int aid_query_pcm(aid_engine *e, const float *pcm, const int64_t *offsets, int32
     // one critical section: no other thread's extraction can land between this batch's K1-K3 and K5
     std::lock_guard<std::mutex> lk(e->mu);
     if (int rc = ensure_index(e)) return rc;
-    if (int rc = extract_locked(e, pcm, offsets, n_clips, loc, stream)) return rc;
-    return query_extracted_locked(e, rows, nrows);
+    if (int rc = extract_locked(e, pcm, offsets, n_clips, loc, stream)) return drain_host_copy(e, loc, stream, rc);
+    return drain_host_copy(e, loc, stream, query_extracted_locked(e, rows, nrows));
 }
 
 }  // extern "C"
@@ -2090,6 +2099,9 @@ extern "C" int aid_exact_windows(int64_t n, int32_t sample_rate, int64_t *lo, in
     return 3;
 }
 
+static int exact_lane_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
+                             int32_t max_out, aid_exact_row *out, int32_t *n_out, void *stream);
+
 extern "C" int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
                               int32_t max_out, aid_exact_row *out, int32_t *n_out, void *stream) {
     if (!e || !offsets || n_clips < 0 || max_out <= 0 || (n_clips > 0 && (!out || !n_out)))
@@ -2102,6 +2114,11 @@ extern "C" int aid_exact_lane(aid_engine *e, const float *pcm, const int64_t *of
     if (e->cfg.max_results > 256) return fail(AID_ERR_INVALID, "aid_exact_lane: engine max_results must be <= 256");
     if (n_clips == 0) return AID_OK;
     std::lock_guard<std::mutex> lk(e->mu);
+    return drain_host_copy(e, loc, stream, exact_lane_locked(e, pcm, offsets, n_clips, loc, max_out, out, n_out, stream));
+}
+
+static int exact_lane_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
+                             int32_t max_out, aid_exact_row *out, int32_t *n_out, void *stream) {
     HIP_TRY(hipSetDevice(e->device));
     if (int rc = ensure_index(e)) return rc;
     hipStream_t s = pick_stream(e, stream);

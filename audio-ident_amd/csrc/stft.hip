@@ -96,16 +96,19 @@ __device__ __forceinline__ void pstore(float *p, float v) {
 #ifndef AID_K1_NTLOAD
 #define AID_K1_NTLOAD 1
 #endif
+// A clip may start at an odd sample (device clips, the exact lane's in-place sub-windows), so a frame's sample
+// pairs are only 4-byte aligned: they are read through a 2-float vector type declared 4-byte aligned (the same
+// global_load_dwordx2; a float2 pointer would promise the compiler 8 bytes)
+typedef float aid_f2u __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ float2 pcm_ld(const aid_f2u &r) {
 #if AID_K1_NTLOAD
-typedef float aid_f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float2 pcm_nt(const float2 &r) {
-    const aid_f2v v = __builtin_nontemporal_load(reinterpret_cast<const aid_f2v *>(&r));
+    const aid_f2u v = __builtin_nontemporal_load(&r);
+#else
+    const aid_f2u v = r;
+#endif
     return make_float2(v.x, v.y);
 }
-#define AID_PCM(ref) pcm_nt(ref)
-#else
-#define AID_PCM(ref) (ref)
-#endif
+#define AID_PCM(ref) pcm_ld(ref)
 
 __device__ __forceinline__ int e3q_slot(int k) { return 4 * (k & 255) + ((k >> 8) ^ (2 * ((k >> 3) & 1))); }
 
@@ -186,7 +189,7 @@ __global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__r
     }
     const int64_t t0 = f - clips[lo].frame_base;
     const int nfr = (int)min(f_end - f, clips[lo].frames - t0);
-    const float2 *src = reinterpret_cast<const float2 *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + e1_perm(lane);
+    const aid_f2u *src = reinterpret_cast<const aid_f2u *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + e1_perm(lane);
     float *dst = out + (clips[lo].frame_base + t0) * kBins;
     uint64_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
 

@@ -102,6 +102,19 @@ def load_pmc() -> tuple[dict, str | None]:
     return {}, None
 
 
+def load_pmc_k5() -> tuple[dict | None, str | None]:
+    """The K5 (config-4 match) summary of the newest committed PMC file that has one (tools/k5_pmc_summary.py):
+    HBM bytes and kernel time per exact-lane call, per K5 kernel and in sum."""
+    for f in sorted((ROOT / "profiles").glob("pmc_*.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        if isinstance(d.get("k5"), dict):
+            return d["k5"], f.name
+    return None, None
+
+
 def load_sq() -> tuple[dict, str | None]:
     """SQ_INSTS_VALU (and the rest) per launch from the newest committed SQ summary (sq_*.txt lines
     `<dir> <kernel> <counter> n= <n> mean=<v>`): {kernel: {counter: mean}}."""
@@ -462,11 +475,19 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     a = types.SimpleNamespace(batch=batch, sr=SR)
     cat = CATEGORIES["noise20"]
 
+    # clips checked against the oracle after the timed region: negatives and positives of the timed calls
+    prng = np.random.default_rng(2000 + rank)
+    n_chk = min(args.lane_parity_clips, n)
+    n_chk_neg = min(n_neg, max(1, n_chk // 8)) if n_chk else 0
+    sel = np.sort(np.concatenate([prng.choice(n_pos, min(n_pos, n_chk - n_chk_neg), replace=False),
+                                  n_pos + prng.choice(n_neg, n_chk_neg, replace=False)]).astype(np.int64))
+
     def local():
         pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
         w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a 4096-clip call is sized here
         run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
-        res, t_gpu = run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, True)
+        res, t_gpu = run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, True, keep=sel)
+        kept = res.pop("kept", {})
         # untimed: the same clips again with events on the K5 kernels and the posting counters
         eng.match_stats(reset=True)
         eng.profile_select(None)
@@ -477,25 +498,172 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
         eng.profile_enable(False)
         ms = eng.match_stats(reset=True)
         del pcm
-        return res, t_gpu, prof, ms
+        par = lane_parity(eng, truth, starts, n_pos, sel, kept, cat, torch) if len(sel) else None
+        return res, t_gpu, prof, ms, par
 
-    res, t_gpu, prof, ms = _agreed(local, "exact lane", dist)
+    res, t_gpu, prof, ms, par = _agreed(local, "exact lane", dist)
     t_max = _max_over_ranks(t_gpu, dist, torch)
     k5_s = sum(prof[k][0] for k in K5_KERNELS if k in prof) * 1e-3
-    alg = 8 * ms["posting_reads"] + 8 * ms["records"]
+    # algorithmic bytes: every vote reads its 8-B posting ONCE, every query record is read once. The LDS path's
+    # second (insert) pass and the global path's per-partition re-reads are the implementation's, not the
+    # algorithm's: they are reported as issued_bytes, and the bytes that reach HBM come from the PMC passes
+    alg = 8 * ms["votes"] + 8 * ms["records"]
+    issued = 8 * ms["posting_reads"] + 8 * ms["records"]
+    pmc_k5, pmc_src = load_pmc_k5()
     roof = {"kernels": list(K5_KERNELS), "bound": "hbm", "unit": "GB/s", "peak": PEAK,
-            "algorithmic_bytes": alg, "k5_seconds": round(k5_s, 4),
+            "algorithmic_bytes": alg, "issued_bytes": issued, "k5_seconds": round(k5_s, 4),
             "achieved": round(alg / k5_s / 1e9, 1) if k5_s else None,
             "frac": round(alg / k5_s / 1e9 / PEAK, 4) if k5_s else None,
+            "issued_frac": round(issued / k5_s / 1e9 / PEAK, 4) if k5_s else None,
             "per_kernel_ms": {k: round(prof[k][0], 3) for k in K5_KERNELS if k in prof and prof[k][1]},
+            "pmc": pmc_k5, "pmc_source": pmc_src,
             "source": "rank 0, untimed second pass of the same clips with HIP events on the K5 kernels",
-            "note": "bytes = 8 B x postings K5 read (LDS path twice per vote (counting and insert passes), global path once per K5a key partition "
-                    "+ once in K5b) + 8 B x query records; the vote histogram's atomics and the exact tables stay "
-                    "in LDS / the caches and are not counted"}
+            "note": "algorithmic bytes = 8 B x votes (one posting read per vote) + 8 B x query records; issued bytes "
+                    "count the LDS path's two enumerations (counting, insert) and the global path's re-reads; the "
+                    "vote filters and exact tables stay in LDS / the caches and are not counted; pmc = the K5 "
+                    "kernels' HBM bytes per config-4 lane call (2 x FETCH_SIZE + WRITE_SIZE) from the newest "
+                    "committed K5 PMC summary"}
+    if pmc_k5 and pmc_k5.get("hbm_bytes_per_call") and pmc_k5.get("k5_ms_per_call"):
+        roof["traffic_frac"] = round(pmc_k5["hbm_bytes_per_call"] / (pmc_k5["k5_ms_per_call"] * 1e-3) / 1e9 / PEAK, 4)
     return {"value": round(world * n / t_max, 1), "unit": "clips/s", "clips_per_rank": n, "positives_per_rank": n_pos,
             "negatives_per_rank": n_neg, "gpu_s_max_over_ranks": round(t_max, 4),
             "category": "noise20 (SNR 20 dB, gain 0.5)", "rank0": res, "match_stats": ms, "roofline": roof,
-            "path": "aid_exact_lane, 4096 clips per call, 3 sub-windows each"}
+            "parity": par, "path": "aid_exact_lane, 4096 clips per call, 3 sub-windows each"}
+
+
+def _oracle_subset(eng, hashes: np.ndarray, torch, chunk: int = 1 << 26) -> np.ndarray:
+    """The index's stored postings whose hash is one of `hashes`, as a host [m, 3] uint32 (hash, track, t) array
+    sorted for fp_query. The planes are exported to the device chunk by chunk (aid_index_export) and filtered
+    there (a sorted-table lookup per posting), so only the few postings the sampled queries can vote through
+    reach the host. Exact for voting: a query touches only postings whose hash equals one of its records'."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # checker only
+
+    q = torch.from_numpy(np.unique(hashes.astype(np.uint32)).view(np.int32).copy()).cuda()
+    q, _ = torch.sort(q)  # int32 order of the uint32 bits: the same order on both sides of the lookup
+    total = eng.index_stats()["postings"]
+    n = min(chunk, max(total, 1))
+    planes = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(3)]
+    parts = []
+    for o in range(0, total, chunk):
+        c = min(chunk, total - o)
+        eng.index_export_device(*(p.data_ptr() for p in planes), o, c)
+        h = planes[0][:c]
+        i = torch.searchsorted(q, h).clamp_(max=len(q) - 1)
+        m = q[i] == h
+        parts.append(torch.stack([p[:c][m] for p in planes], dim=1).cpu().numpy().view(np.uint32))
+    del planes
+    sub = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros((0, 3), np.uint32))
+    O.lib().fp_index_sort(O._ptr(sub), len(sub))
+    return sub
+
+
+def lane_parity(eng, truth, starts, n_pos: int, sel, kept: dict, cat, torch) -> dict:
+    """Config 4 pinned at its configured scale: for the sampled clips `sel` of the timed
+    exact-lane calls, against the whole catalog index (reference app/audio/fingerprint.py:185-202,
+    app/search/exact.py:132-293):
+      * window records: the engine's extraction of each sub-window equals oracle/fp_oracle.c's;
+      * K5 rows: aid_query over the oracle's window records, on the LDS path, the global path and the automatic
+        choice, equals oracle/fp_match.c fp_query over the index's postings with those hashes (every vote the
+        query can cast) -- count, track, d, tq_min, tq_max, order;
+      * the lane: the rows aid_exact_lane returned in the timed 4096-clip calls equal an all-oracle lane -- the
+        oracle's records, fp_query, then aidfp.exact.run_exact_lane's per-window path (the reference's
+        sub-window slicing, consensus, MIN_ALIGNED_HASHES, confidence and stable rank, pinned to reference
+        vectors by tests/test_glue_parity.py): tracks, aligned counts, binary64 offsets and confidences, order.
+    Checker only: runs after the timed region."""
+    import asyncio
+    import ctypes
+    import uuid
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # checker only
+    from aidfp import exact as ex
+    from aidfp import synth
+    from aidfp.engine import exact_windows
+    from aidfp.fingerprint import OlafMatch
+    from bench_match import _apply
+
+    t0 = time.perf_counter()
+    clip_n = 5 * SR
+    m = len(sel)
+    pcm = torch.empty(m * clip_n, dtype=torch.float32, device="cuda")
+    # the sampled clips exactly as the timed calls generated them (same synth arguments, same degradation)
+    eng.synth(pcm.data_ptr(), truth[sel], starts[sel], clip_n, noise_a=synth.noise_halfwidth(cat["snr"]), salt=77)
+    _apply(pcm, m, clip_n, cat["gain"], cat["band"], SR)
+    host = pcm.view(m, clip_n).cpu().numpy()
+    del pcm
+    _, plan = exact_windows(clip_n, SR)
+    # the reference's own slicing of each clip (exact.py:150-160) must be the engine's window plan
+    clip_bytes = [host[i].astype("<f4").tobytes() for i in range(m)]
+    pieces = []
+    for i in range(m):
+        for w, (a, b) in enumerate(ex.SUB_WINDOWS):
+            pc = ex.extract_pcm_window(clip_bytes[i], a, min(b, ex.pcm_duration_sec(clip_bytes[i], SR)), SR)
+            lo, ln = plan[w]
+            if pc != host[i, lo:lo + ln].astype("<f4").tobytes():
+                return {"clips": m, "rows_bit_exact": False, "lane_equal": False,
+                        "error": f"window plan differs from the reference slicing (clip {i}, window {w})"}
+            pieces.append(pc)
+    wins = [np.frombuffer(pc, dtype="<f4").astype(np.float32) for pc in pieces]
+    threads = max(1, min(16, cpu_info()["cores"]))
+    with ThreadPoolExecutor(threads) as pool:
+        recs = list(pool.map(lambda x: O.fingerprint(x, eng.hop), wins))
+    got = eng.extract_host(wins)
+    records_ok = all(np.array_equal(g, r) for g, r in zip(got, recs))
+    sub = _oracle_subset(eng, np.concatenate([r & np.uint64(0xFFFFFFFF) for r in recs]), torch)
+    t_sub = time.perf_counter() - t0
+
+    def fp_rows(r: np.ndarray) -> np.ndarray:
+        qh = np.ascontiguousarray((r & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+        qt = np.ascontiguousarray((r >> np.uint64(32)).astype(np.uint32))
+        out = (O.Row * eng.max_results)()
+        k = int(O.lib().fp_query(O._ptr(sub), len(sub), O._ptr(qh), O._ptr(qt), len(r), eng.min_match,
+                                 ctypes.addressof(out), eng.max_results))
+        return np.array([[x.match_count, x.track, x.d, x.tq_min, x.tq_max] for x in out[:k]],
+                        dtype=np.int64).reshape(-1, 5)
+
+    with ThreadPoolExecutor(threads) as pool:
+        oracle_rows = list(pool.map(fp_rows, recs))
+    paths = {}
+    for name, force in (("auto", 0), ("lds", 1), ("global", 2)):
+        eng.match_stats(reset=True)
+        eng.force("k5_path", force)
+        try:
+            rows = eng.query(recs)
+        finally:
+            eng.force("k5_path", 0)
+        st = eng.match_stats(reset=True)
+        bad = [i for i, (a, b) in enumerate(zip(rows, oracle_rows)) if not np.array_equal(a, b)]
+        paths[name] = {"bit_exact": not bad, "mismatched_windows": bad[:8], "queries_lds": st["queries_lds"],
+                       "queries_global": st["queries_global"]}
+    by_piece = dict(zip(pieces, oracle_rows))
+    sec = eng.hop / SR
+
+    async def oracle_query(piece: bytes):
+        return [OlafMatch(int(c), tq0 * sec, tq1 * sec, str(uuid.UUID(int=int(tr) + 1)), int(tr), (tq0 + d) * sec,
+                          (tq1 + d) * sec) for c, tr, d, tq0, tq1 in by_piece[piece].tolist()]
+
+    lane_bad = []
+    for i, q in enumerate(sel):
+        want = asyncio.run(ex.run_exact_lane(clip_bytes[i], 10, query=oracle_query, sample_rate=SR))
+        r = kept[int(q)]
+        same = len(r) == len(want) and all(
+            int(x["track"]) == w.track.int - 1 and int(x["aligned_hashes"]) == w.aligned_hashes
+            and float(x["offset_seconds"]) == w.offset_seconds and float(x["confidence"]) == w.confidence
+            for x, w in zip(r, want))
+        if not same:
+            lane_bad.append(int(q))
+    votes = [int(sum(np.searchsorted(sub[:, 0], h, "right") - np.searchsorted(sub[:, 0], h, "left")
+                     for h in (r & np.uint64(0xFFFFFFFF)).astype(np.uint32))) for r in recs[:3]]
+    return {"clips": m, "windows": len(recs), "negatives": int(sum(int(q) >= n_pos for q in sel)),
+            "records_bit_exact": records_ok, "rows_bit_exact": all(p["bit_exact"] for p in paths.values()),
+            "k5_paths": paths, "lane_equal": not lane_bad, "lane_mismatched_clips": lane_bad[:8],
+            "index_postings": int(eng.index_stats()["postings"]), "oracle_subset_postings": int(len(sub)),
+            "votes_first_windows": votes, "seconds": round(time.perf_counter() - t0, 2),
+            "subset_seconds": round(t_sub, 2),
+            "oracle": "oracle/fp_oracle.c records, oracle/fp_match.c fp_query over the index postings with the "
+                      "windows' hashes, aidfp.exact.run_exact_lane (per-window path) for the consensus"}
 
 
 def service_leg(args, rank, world, dist, torch) -> dict:
@@ -623,6 +791,8 @@ def main() -> int:
     ap.add_argument("--exact-clips", type=int, default=10000,
                     help="config-4 positive query clips per rank against the catalog leg's index, plus 10 %% "
                          "negatives from unseen tracks (BASELINE configs[3]: 10k; 0 = skip)")
+    ap.add_argument("--lane-parity-clips", type=int, default=64,
+                    help="exact-lane clips per rank checked against the oracle at the catalog's scale (0 = none)")
     ap.add_argument("--no-service", action="store_true", help="skip the drop-in service leg")
     ap.add_argument("--service-tracks", type=int, default=10000)
     ap.add_argument("--service-requests", type=int, default=512)
@@ -786,6 +956,7 @@ def main() -> int:
     # A leg that never returns (a collective stuck on some rank) must not cost the headline line: past the deadline a
     # watchdog prints the line with the unfinished legs marked and ends the process (every rank runs the same timer)
     legs = {"catalog": None, "service": None}
+    stage = ["catalog"]  # the leg running now, for the watchdog's report
     emitted = threading.Lock()
     finished = threading.Event()
 
@@ -799,20 +970,31 @@ def main() -> int:
     def watchdog():
         if finished.wait(args.leg_deadline):
             return
-        for k in legs:
-            if legs[k] is None and not getattr(args, f"no_{k}"):
-                legs[k] = {"error": f"deadline: not finished {args.leg_deadline:.0f} s after the headline"}
-        _log("leg deadline passed: printing the line without the unfinished legs and exiting")
+        hung = [k for k in legs if legs[k] is None and not getattr(args, f"no_{k}")]
+        for k in hung:
+            legs[k] = {"error": f"deadline: not finished {args.leg_deadline:.0f} s after the headline",
+                       "stopped_in": stage[0]}
+        _log(f"leg deadline passed in {stage[0]!r} (unfinished: {', '.join(hung)}): printing the line without them "
+             "and exiting non-zero")
         if emit_line():
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0 if ok_headline() else 1)
+            # a hung leg is a failed run (exit 3), whatever the headline measured; 1 if the headline failed parity
+            os._exit(1 if not ok_headline() else 3)
 
     def ok_headline() -> bool:
         ok = par is None or par["bit_exact"]
         if fullband and "parity" in fullband:
             ok = ok and fullband["parity"]["bit_exact"]
         return ok
+
+    def ok_lane() -> bool:
+        """The config-4 lane's parity at the catalog's scale (catalog.exact_lane.parity), when it ran."""
+        lane = (legs["catalog"] or {}).get("exact_lane") or {}
+        lp = lane.get("parity")
+        if not lp:
+            return True
+        return bool(lp.get("records_bit_exact") and lp.get("rows_bit_exact") and lp.get("lane_equal"))
 
     def make_line(catalog, service) -> dict:
         return {
@@ -861,6 +1043,7 @@ def main() -> int:
         legs["catalog"] = catalog
 
     _log("catalog + exact lane done")
+    stage[0] = "service"
     service = None
     if not args.no_service:
         try:  # service_leg agrees on its rank-local parts, so every rank takes this branch alike
@@ -870,12 +1053,16 @@ def main() -> int:
         legs["service"] = service
 
     _log("service done")
+    if os.environ.get("AIDFP_DUMP_MAPS"):  # diagnostics: the process's mappings, to symbolise an exit-time trace
+        Path(os.environ["AIDFP_DUMP_MAPS"]).write_text(Path("/proc/self/maps").read_text())
     finished.set()
     if not emit_line():  # the watchdog printed the line and is ending the process
         threading.Event().wait()
     if dist:
         dist.destroy_process_group()
-    return 0 if ok_headline() else 1
+    if not ok_lane():
+        _log("exact-lane parity at the catalog's scale FAILED (catalog.exact_lane.parity)")
+    return 0 if ok_headline() and ok_lane() else 1
 
 
 if __name__ == "__main__":

@@ -167,8 +167,9 @@ CATEGORIES = {
 }
 
 
-def run_batches(args, eng, truth, starts, n_pos, cat, pcm, clip_n, timed: bool):
-    """One category through aid_exact_lane in batches: accuracy counters and, if timed, the GPU seconds."""
+def run_batches(args, eng, truth, starts, n_pos, cat, pcm, clip_n, timed: bool, keep=None):
+    """One category through aid_exact_lane in batches: accuracy counters and, if timed, the GPU seconds.
+    keep: clip indices whose lane rows are returned as well (res["kept"] = {index: rows}), for the parity check."""
     import torch
 
     from aidfp import synth
@@ -178,6 +179,8 @@ def run_batches(args, eng, truth, starts, n_pos, cat, pcm, clip_n, timed: bool):
     t_gpu = 0.0
     top1 = top5 = fp_hits = 0
     off_err = []
+    keep = set() if keep is None else {int(k) for k in keep}
+    kept = {}
     for q0 in range(0, nq, args.batch):
         qs = np.arange(q0, min(nq, q0 + args.batch))
         eng.synth(pcm.data_ptr(), truth[qs], starts[qs], clip_n, noise_a=noise_a, salt=77)
@@ -189,6 +192,8 @@ def run_batches(args, eng, truth, starts, n_pos, cat, pcm, clip_n, timed: bool):
         t_gpu += time.perf_counter() - t1  # aid_exact_lane is synchronous (rows on the host)
         for i, q in enumerate(qs):
             r = rows[i]
+            if int(q) in keep:
+                kept[int(q)] = r.copy()
             if q < n_pos:
                 ids = [int(x) for x in r["track"][:5]]
                 if ids and ids[0] == int(truth[q]):
@@ -202,7 +207,8 @@ def run_batches(args, eng, truth, starts, n_pos, cat, pcm, clip_n, timed: bool):
             "gain_db": round(20 * np.log10(cat["gain"]), 1), "band_hz": cat["band"],
             "top1": round(top1 / max(1, n_pos), 4), "top5": round(top5 / max(1, n_pos), 4),
             "false_positive_rate": round(fp_hits / max(1, n_neg), 4),
-            "median_offset_error_s": round(float(np.median(off_err)), 4) if off_err else None}, t_gpu
+            "median_offset_error_s": round(float(np.median(off_err)), 4) if off_err else None,
+            **({"kept": kept} if keep else {})}, t_gpu
 
 
 def cpu_baseline(args, eng) -> dict:

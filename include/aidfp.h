@@ -114,7 +114,10 @@ int64_t aid_hash_capacity(const aid_engine *e, int64_t n_samples);
  * Clip c is pcm[offsets[c] .. offsets[c+1]); `offsets` is a HOST array of
  * n_clips+1 non-decreasing sample indices. With AID_PCM_DEVICE, `pcm` is a device
  * pointer read in place (a clip at an odd offset reads its frames with 4-byte aligned
- * float2 loads); with AID_PCM_HOST the engine stages the samples itself.
+ * float2 loads); with AID_PCM_HOST the engine stages the samples itself, by ONE
+ * asynchronous copy on `stream`: from page-locked memory that copy is a DMA, so
+ * host PCM must stay unchanged until the call's stream completes (aid_sync, or
+ * any aid_result_* call). An error return has already drained the stream.
  * Asynchronous on `stream`; results stay on the device until fetched below.
  * Replaces the FFT/peak/hash work of `olaf_c store|query` (fingerprint.py:117,185).
  */

@@ -465,6 +465,31 @@ def test_one_failing_request_does_not_blank_its_batch(svc, monkeypatch):
     assert max(calls) > 1  # it was coalesced
 
 
+def test_device_error_fails_the_batch_without_bisecting(svc, monkeypatch):
+    """A device fault (AID_ERR_DEVICE) or an invalid argument does not depend on the batch: the coalesced batch
+    gets [] for every request after ONE engine call, instead of ~2n bisected calls under the shared lock."""
+    import time as _t
+
+    assert run(fp.olaf_index_track(_pcm_of(0.2), uuid.UUID(int=3000)))
+    eng = svc._eng()
+    calls = []
+
+    def broken(clips):
+        calls.append(len(clips))
+        _t.sleep(0.005)
+        raise _lib.EngineError(_lib.AID_ERR_DEVICE, "hipErrorLaunchFailure")
+
+    monkeypatch.setattr(eng, "query_pcm", broken)
+
+    async def many():
+        return await asyncio.gather(*[fp.olaf_query(_pcm_of(0.2)) for _ in range(24)])
+
+    got = run(many())
+    assert got == [[]] * 24
+    assert sum(calls) == 24  # every request was sent exactly once: no retries in halves
+    assert max(calls) > 1  # and the batches were coalesced
+
+
 def test_coalescer_caps_batch_bytes():
     """QueryCoalescer closes a batch before the next payload would pass max_batch_bytes; that payload opens
     the next batch, and one payload above the cap runs alone."""
