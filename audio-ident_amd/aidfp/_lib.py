@@ -110,6 +110,7 @@ SIGNATURES = [
     ("aid_index_stats", ctypes.c_int, [P, P, P, P]),
     ("aid_match_stats", ctypes.c_int, [P, P, I32, I32]),
     ("aid_index_export", ctypes.c_int, [P, P, P, P, I64, I64, I32]),
+    ("aid_index_checksum", ctypes.c_int, [P, I64, I64, P]),
     ("aid_comm_id", ctypes.c_int, [P]),
     ("aid_comm_create", ctypes.c_int, [P, P, I32, I32, P]),
     ("aid_comm_destroy", None, [P]),
@@ -124,12 +125,14 @@ SIGNATURES = [
     ("aid_query", ctypes.c_int, [P, P, P, I32, P, P]),
     ("aid_query_extracted", ctypes.c_int, [P, P, P]),
     ("aid_query_pcm", ctypes.c_int, [P, P, P, I32, I32, P, P, P]),
+    ("aid_query_windows", ctypes.c_int, [P, P, P, P, I32, P, P, P]),
     ("aid_exact_lane", ctypes.c_int, [P, P, P, I32, I32, I32, P, P, P]),
     ("aid_exact_windows", ctypes.c_int, [I64, I32, P, P, P]),
     ("aid_downmix", ctypes.c_int, [P, P, I64, P, P]),
     ("aid_resample_len", I64, [I64, I32, I32]),
     ("aid_resample", ctypes.c_int, [P, P, I64, I32, I32, I32, P, I64, P, P]),
     ("aid_resample_range", ctypes.c_int, [P, P, I64, I64, I32, I32, I32, I64, I64, P, P]),
+    ("aid_resample_batch", ctypes.c_int, [P, P, I64, I32, I64, I64, I32, I32, I32, I64, I64, P, I64, P]),
     ("aid_resample_plan", ctypes.c_int, [I32, I32, P, P, P, P]),
     ("aid_dedup_reset", ctypes.c_int, [P]),
     ("aid_dedup_add", ctypes.c_int, [P, P, P, P, I32]),
@@ -160,8 +163,14 @@ def load() -> ctypes.CDLL:
             L = ctypes.CDLL(str(LIB_PATH))
         except OSError as exc:  # pragma: no cover - depends on the box
             raise EngineUnavailable(f"cannot load {LIB_PATH}: {exc}") from exc
+        ab = "AIDFP_LIB" in os.environ  # an A/B build of an older source tree may lack newer entry points
         for name, res, args in SIGNATURES:
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                if ab:
+                    continue
+                raise
             f.restype = res
             f.argtypes = args
         _lib = L

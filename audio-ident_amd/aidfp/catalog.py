@@ -136,6 +136,43 @@ def exchange_postings(eng, first: int = 0, group=None) -> int:
     return eng.index_splice(first, recv.data_ptr() if stride else 0, counts, stride, tracks)
 
 
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def checksum_np(postings: np.ndarray, first_index: int = 0) -> int:
+    """Host mirror of aid_index_checksum over a [n, 3] uint32 (hash, track, t) array whose row 0 sits at position
+    `first_index` of the checksummed range (tests; the replicas are checksummed on the device)."""
+    p = np.asarray(postings, dtype=np.uint32).reshape(-1, 3).astype(np.uint64)
+    i = np.arange(first_index, first_index + len(p), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = ((p[:, 0] << np.uint64(32)) | p[:, 2]) ^ (p[:, 1] * np.uint64(0x9E3779B97F4A7C15)) ^ \
+            (i * np.uint64(0xD6E8FEB86659FD93))
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return int(np.add.reduce(z, dtype=np.uint64)) if len(z) else 0
+
+
+def replica_check(eng, group=None) -> dict:
+    """Collective: every rank checksums its whole replica on the device (aid_index_checksum) and the checksums
+    are all-gathered; `replicas_identical` is true when every rank holds the same postings in the same order."""
+    import torch.distributed as dist
+
+    def local():
+        return eng.index_checksum(), eng.index_stats()["postings"]
+
+    if dist.is_available() and dist.is_initialized():
+        mine, n = agreed(local, "replica checksum", group)  # a rank that cannot checksum fails every rank
+        allc = [None] * dist.get_world_size(group)
+        dist.all_gather_object(allc, (mine, n), group=group)
+    else:
+        mine, n = local()
+        allc = [(mine, n)]
+    return {"replicas_identical": len({c for c, _ in allc}) == 1 and len({k for _, k in allc}) == 1,
+            "checksum": f"{mine:016x}", "ranks": len(allc),
+            "mismatched_ranks": [r for r, (c, k) in enumerate(allc) if (c, k) != allc[0]]}
+
+
 @dataclass
 class IngestStats:
     tracks_local: int

@@ -328,9 +328,9 @@ class Engine:
 
     def match_stats(self, reset: bool = False) -> dict:
         """Cumulative K5 counters (aid_match_stats): queries, votes, postings read, path split, records."""
-        out = np.zeros(6, dtype=np.int64)
-        check(self._lib.aid_match_stats(self._h, _p(out), 6, 1 if reset else 0))
-        return dict(zip(("queries", "votes", "posting_reads", "queries_lds", "queries_global", "records"),
+        out = np.zeros(7, dtype=np.int64)
+        check(self._lib.aid_match_stats(self._h, _p(out), 7, 1 if reset else 0))
+        return dict(zip(("queries", "votes", "posting_reads", "queries_lds", "queries_global", "records", "sig_reads"),
                         (int(x) for x in out)))
 
     # ---- PCM front-end (FPSPEC 8): downmix + resample, device buffers ----
@@ -353,6 +353,15 @@ class Engine:
         check(self._lib.aid_resample_range(self._h, ctypes.c_void_p(src_ptr), int(in_base), int(n), int(channels),
                                            int(sr_in), int(sr_out), int(m_first), int(count),
                                            ctypes.c_void_p(dst_ptr), ctypes.c_void_p(stream) if stream else None))
+
+    def resample_batch(self, src_ptr: int, src_stride: int, n_streams: int, in_base: int, n: int, channels: int,
+                       sr_in: int, sr_out: int, m_first: int, count: int, dst_ptr: int, dst_stride: int,
+                       stream: int | None = None) -> None:
+        """resample_range for n_streams lockstep streams in one launch (strides in floats; aid_resample_batch)."""
+        check(self._lib.aid_resample_batch(self._h, ctypes.c_void_p(src_ptr), int(src_stride), int(n_streams),
+                                           int(in_base), int(n), int(channels), int(sr_in), int(sr_out), int(m_first),
+                                           int(count), ctypes.c_void_p(dst_ptr), int(dst_stride),
+                                           ctypes.c_void_p(stream) if stream else None))
 
     def resample_plan(self, sr_in: int, sr_out: int):
         v = [ctypes.c_int32() for _ in range(4)]
@@ -423,6 +432,13 @@ class Engine:
         check(self._lib.aid_index_export(self._h, _p(cols[0]), _p(cols[1]), _p(cols[2]), first, count, AID_PCM_HOST))
         return np.stack([c[:count] for c in cols], axis=1)
 
+    def index_checksum(self, first: int = 0, count: int | None = None) -> int:
+        """aid_index_checksum: order-sensitive 64-bit checksum of stored postings [first, first+count) (device)."""
+        count = self.index_stats()["postings"] - first if count is None else count
+        out = ctypes.c_uint64(0)
+        check(self._lib.aid_index_checksum(self._h, int(first), int(count), ctypes.byref(out)))
+        return int(out.value)
+
     def index_export_device(self, hash_ptr: int, track_ptr: int, t_ptr: int, first: int, count: int) -> None:
         check(self._lib.aid_index_export(self._h, ctypes.c_void_p(hash_ptr), ctypes.c_void_p(track_ptr),
                                          ctypes.c_void_p(t_ptr), first, count, AID_PCM_DEVICE))
@@ -475,6 +491,20 @@ class Engine:
         nrows = np.zeros(nq, dtype=np.int32)
         check(self._lib.aid_query_pcm(self._h, _p(pcm), _p(offsets), nq, AID_PCM_HOST, ctypes.addressof(rows),
                                       _p(nrows), None))
+        self.n_clips = nq
+        return self._rows(rows, nrows, nq)
+
+    def query_windows(self, pcm_ptr: int, starts, ends, stream: int | None = None) -> list[np.ndarray]:
+        """Extract + match device-PCM windows [starts[c], ends[c]) (may overlap) in one engine call."""
+        st = np.ascontiguousarray(starts, dtype=np.int64)
+        en = np.ascontiguousarray(ends, dtype=np.int64)
+        nq = len(st)
+        if nq == 0:
+            return []
+        rows = (AidMatchRow * (nq * self.max_results))()
+        nrows = np.zeros(nq, dtype=np.int32)
+        check(self._lib.aid_query_windows(self._h, ctypes.c_void_p(pcm_ptr), _p(st), _p(en), nq, ctypes.addressof(rows),
+                                          _p(nrows), ctypes.c_void_p(stream) if stream else None))
         self.n_clips = nq
         return self._rows(rows, nrows, nq)
 

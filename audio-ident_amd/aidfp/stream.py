@@ -17,6 +17,7 @@ engine call (K1-K3 + K5) against the index.
 
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -168,3 +169,119 @@ class StreamIdentifier:
     def mono_history(self) -> np.ndarray:
         """Host copy of the mono buffer (index rate) currently held, from stream sample self.base."""
         return self.mono[: self.filled].cpu().numpy()
+
+
+class StreamBank:
+    """S live streams identified in lockstep (BASELINE config 5 at serving scale).
+
+    Every push hands over the same length of interleaved stereo for every stream ([S, n, 2] float32, a device
+    tensor or a host array). Per push the whole bank costs ONE K6 launch (aid_resample_batch: downmix + polyphase
+    resampling of all S streams, each keeping its own filter history, so chunked output equals whole-signal
+    resampling bit for bit) and ONE extraction + match call over every window the push completed in every stream
+    (aid_query_windows: K1-K3 read the 50 %-overlap windows in place from the streams' mono buffers, then K5).
+    The reference's equivalent is one ffmpeg process and one `olaf_c query` per recorded clip
+    (audio-ident-ui AudioRecorder.svelte:86-106 -> app/audio/decode.py:41-60 -> app/audio/fingerprint.py:158-219).
+    """
+
+    def __init__(self, engine, n_streams: int, stream_sr: int = 48000, window_s: float = 5.0, hop_s: float = 2.5,
+                 capacity_s: float = 30.0):
+        import torch
+
+        self.eng = engine
+        self.S = int(n_streams)
+        self.sr = engine.sample_rate
+        self.stream_sr = int(stream_sr)
+        if self.stream_sr == self.sr:
+            raise ValueError("StreamBank resamples: the stream rate must differ from the index rate "
+                             "(StreamIdentifier handles same-rate streams)")
+        self.win = int(round(window_s * self.sr)) & ~1
+        self.hop = int(round(hop_s * self.sr)) & ~1
+        self.up, self.down, self.hl, self.J = engine.resample_plan(self.stream_sr, self.sr)
+        self.cap_in = max(int(capacity_s * self.stream_sr), 4 * int(window_s * self.stream_sr)) & ~1
+        self.cap_m = max(int(capacity_s * self.sr), 4 * self.win) & ~1
+        self.raw = torch.zeros(self.S, 2 * self.cap_in, dtype=torch.float32, device="cuda")  # [stream][frame][L, R]
+        self.mono = torch.zeros(self.S, self.cap_m, dtype=torch.float32, device="cuda")
+        self._pin = None
+        self.raw_base = 0    # stream frame (stream rate) of raw[:, 0]
+        self.raw_filled = 0  # frames held per stream
+        self.n_in = 0        # frames received per stream
+        self.m_next = 0      # next mono sample (index rate) to produce
+        self.base = 0        # stream sample (index rate) of mono[:, 0]
+        self.filled = 0
+        self.next_start = 0  # stream sample of the next window
+        self.timings = None  # a list: push() appends (append, resample, windows) host seconds per push (bench)
+
+    def _append_raw(self, chunk, n: int) -> None:
+        import torch
+
+        if self.raw_filled + n > self.cap_in:  # compact: keep the input the next output still reads
+            need = max(self.raw_base, (self.m_next * self.down + self.hl) // self.up - (self.J - 1))
+            drop = need - self.raw_base
+            keep = self.raw_filled - drop
+            if keep + n > self.cap_in:
+                raise ValueError("chunk larger than the stream buffer")
+            src = self.raw[:, 2 * drop: 2 * self.raw_filled]
+            self.raw[:, : 2 * keep] = src if keep <= drop else src.clone()  # no overlap: no temporary copy
+            self.raw_base += drop
+            self.raw_filled = keep
+        dst = self.raw[:, 2 * self.raw_filled: 2 * (self.raw_filled + n)]
+        if isinstance(chunk, torch.Tensor):
+            dst.copy_(chunk.reshape(self.S, 2 * n), non_blocking=True)
+        else:  # host chunk: through a page-locked staging buffer (an async DMA); synced before its next refill
+            x = np.ascontiguousarray(chunk, dtype=np.float32).reshape(self.S, 2 * n)
+            if self._pin is None or self._pin.numel() < x.size:
+                self._pin = torch.empty(x.size, dtype=torch.float32).pin_memory()
+            torch.cuda.current_stream().synchronize()  # the previous chunk has left the staging buffer
+            pin = self._pin[: x.size].view(self.S, 2 * n)
+            pin.numpy()[:] = x
+            dst.copy_(pin, non_blocking=True)
+        self.raw_filled += n
+        self.n_in += n
+
+    def push(self, chunk) -> list[list[WindowResult]]:
+        """chunk: [S, n, 2] float32 at stream_sr (device tensor or host array). Returns, per stream, the windows this
+        push completed (the same start times in every stream)."""
+        import torch
+
+        n = int(chunk.shape[1])
+        if chunk.shape[0] != self.S or (len(chunk.shape) > 2 and chunk.shape[2] != 2):
+            raise ValueError("chunk must be [n_streams, n, 2]")
+        s = torch.cuda.current_stream().cuda_stream
+        t0 = time.perf_counter()
+        if n:
+            self._append_raw(chunk, n)
+        t1 = time.perf_counter()
+        last = self.n_in * self.up - 1 - self.hl  # outputs m whose last input floor((m*down + hl)/up) has arrived
+        m_ready = last // self.down + 1 if last >= 0 else 0
+        count = m_ready - self.m_next
+        if count > 0:
+            if self.filled + count > self.cap_m:  # compact: keep what pending windows still need
+                drop = (self.next_start - self.base) & ~1
+                keep = self.filled - drop
+                if keep + count > self.cap_m:
+                    raise ValueError("chunk larger than the stream buffer")
+                src = self.mono[:, drop: self.filled]
+                self.mono[:, :keep] = src if keep <= drop else src.clone()
+                self.base += drop
+                self.filled = keep
+            self.eng.resample_batch(self.raw.data_ptr(), 2 * self.cap_in, self.S, self.raw_base, self.raw_filled, 2,
+                                    self.stream_sr, self.sr, self.m_next, count,
+                                    self.mono.data_ptr() + 4 * self.filled, self.cap_m, s)
+            self.filled += count
+            self.m_next = m_ready
+        t2 = time.perf_counter()
+        starts = []
+        while self.next_start + self.win <= self.base + self.filled:
+            starts.append(self.next_start)
+            self.next_start += self.hop
+        if not starts:
+            if self.timings is not None:
+                self.timings.append((t1 - t0, t2 - t1, 0.0))
+            return [[] for _ in range(self.S)]
+        rel = np.array(starts, dtype=np.int64) - self.base
+        ws = (np.arange(self.S, dtype=np.int64)[:, None] * self.cap_m + rel[None, :]).ravel()
+        rows = self.eng.query_windows(self.mono.data_ptr(), ws, ws + self.win, s)
+        if self.timings is not None:
+            self.timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
+        k = len(starts)
+        return [[WindowResult(st / self.sr, rows[i * k + j]) for j, st in enumerate(starts)] for i in range(self.S)]

@@ -67,6 +67,14 @@ __host__ __device__ constexpr uint32_t bucket_key(uint32_t h) {
            (h & 0x3Fu);
 }
 
+// K5 posting signature (2 B per posting, stored beside the CSR's 8-B posting by K4): sig = H(track) + t mod 2^16.
+// A query's vote on that posting has d = t - tq, so (sig - tq) mod 2^16 = H(track) + d mod 2^16 is a hash of
+// (track, d) that needs neither of them: the LDS match path counts its votes from the 2-B signatures alone and
+// reads the 8-B posting only for votes whose bucket turns out hot (any hash keeps the filter an exact superset).
+__host__ __device__ constexpr uint16_t posting_sig(uint32_t track, uint32_t t) {
+    return (uint16_t)(((track * 0x9E3779B1u) >> 16) + t);
+}
+
 // K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
 constexpr int kHashChunk = 1024;
 constexpr int kHashChunkPeakCap = 64 * ((kHashChunk + kZoneDT + 7) / 8);

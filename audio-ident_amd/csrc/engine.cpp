@@ -35,7 +35,8 @@ void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int
                   int noise_a, uint32_t salt, int fmax_hz, bool envelope, const int16_t *sin_tab, hipStream_t s);
 int64_t resample_lds_floats(int up, int down, int J);
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
-                     const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s);
+                     const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s, int n_streams = 1,
+                     int64_t src_stride = 0, int64_t dst_stride = 0);
 int dedup_chunks(int64_t n_cat);
 void launch_dedup_scan(const uint32_t *cw, const int64_t *coff, const double *cdur, int64_t n_cat, const uint32_t *qw,
                        const int64_t *qoff, const double *qlo, const double *qhi, int nq, double *part_sim,
@@ -53,7 +54,8 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
                                    uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
                                    uint32_t *scratch, uint32_t *E, uint32_t *offsets, unsigned long long *nz,
-                                   uint64_t **vals_out, hipStream_t s);
+                                   uint64_t **vals_out, uint16_t *sig, hipStream_t s);
+void launch_make_sig(const uint64_t *post, int64_t n, uint16_t *sig, hipStream_t s);
 void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
                     uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
                     uint32_t *ot, hipStream_t s);
@@ -67,10 +69,12 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
                   int parts, int stage, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
+void launch_index_checksum(const uint32_t *ph, const uint32_t *ptr, const uint32_t *pt, int64_t first, int64_t n,
+                           unsigned long long *out, hipStream_t s);
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
                       int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, const int64_t *votes,
-                      hipStream_t s);
+                      const uint16_t *sig, hipStream_t s);
 uint32_t index_keys();
 void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
 void launch_window_gather(const float *src, const int64_t *win, int n_win, int64_t max_len, float *dst, hipStream_t s);
@@ -168,6 +172,7 @@ struct aid_engine {
     uint32_t n_tracks = 0;        // max track id + 1
     DevBuf<uint32_t> idx_cnt, idx_off, scan_tmp;
     DevBuf<uint64_t> idx_post;
+    DevBuf<uint16_t> idx_sig;  // K5's 2-B vote signature per CSR posting (aidfp_layout.h posting_sig)
     DevBuf<uint32_t> srt_k0, srt_k1;  // K4 sort build: key double buffer
     DevBuf<uint64_t> srt_v;           // K4 sort build: the value buffer idx_post pairs with
     DevBuf<uint8_t> srt_tmp;          // K4 rocPRIM build (A/B): its temporary storage
@@ -178,6 +183,7 @@ struct aid_engine {
     int64_t n_buckets_used = 0;
     int64_t n_fallback = 0;  // queries answered by the global-histogram path
     DevBuf<unsigned long long> nz;
+    DevBuf<unsigned long long> chk;  // aid_index_checksum result
     // query workspaces
     DevBuf<uint64_t> q_recs;
     DevBuf<int64_t> q_start, q_count;
@@ -228,6 +234,7 @@ struct aid_engine {
     bool k5_spec_ok = true;  // the previous query batch's heaviest query fitted the LDS path (speculation gate)
     // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
     int64_t st_queries = 0, st_votes = 0, st_post_reads = 0, st_q_global = 0, st_q_lds = 0, st_records = 0;
+    int64_t st_sig_reads = 0;  // 2-B posting signatures the LDS path read (two per vote: counting and insert passes)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     size_t k5_batch = 2048;        // global-path queries per launch
     hipStream_t last_stream = nullptr;
@@ -443,6 +450,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->idx_off.release();
     e->scan_tmp.release();
     e->idx_post.release();
+    e->idx_sig.release();
     e->srt_k0.release();
     e->srt_k1.release();
     e->srt_v.release();
@@ -483,6 +491,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->g_send.release();
     e->g_recv.release();
     e->x_tracks.release();
+    e->chk.release();
     if (e->h_desc) (void)hipHostFree(e->h_desc);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->desc_ev) (void)hipEventDestroy(e->desc_ev);
@@ -907,8 +916,18 @@ static int resample_taps_dev(aid_engine *e, const ResamplePlan &p, float **out) 
 
 int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t n, int32_t channels, int32_t sr_in,
                        int32_t sr_out, int64_t m_first, int64_t count, float *dst, void *stream) {
-    if (!e || n < 0 || in_base < 0 || m_first < 0 || count < 0 || (channels != 1 && channels != 2))
+    return aid_resample_batch(e, src, 0, 1, in_base, n, channels, sr_in, sr_out, m_first, count, dst, 0, stream);
+}
+
+int aid_resample_batch(aid_engine *e, const float *src, int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n,
+                       int32_t channels, int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
+                       int64_t dst_stride, void *stream) {
+    if (!e || n < 0 || in_base < 0 || m_first < 0 || count < 0 || (channels != 1 && channels != 2) || n_streams < 0 ||
+        n_streams > 65535 || src_stride < 0 || dst_stride < 0)
         return fail(AID_ERR_INVALID, "aid_resample: bad argument");
+    if (n_streams > 1 && (src_stride < n * channels || dst_stride < count || (channels == 2 && (src_stride & 1))))
+        return fail(AID_ERR_INVALID, "aid_resample_batch: strides must cover one stream (stereo: even)");
+    if (n_streams == 0) return AID_OK;
     ResamplePlan p;
     if (!resample_plan(sr_in, sr_out, p)) return fail(AID_ERR_INVALID, "aid_resample: sample rates must be > 0");
     if (count == 0) return AID_OK;
@@ -925,7 +944,8 @@ int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t
     if (int rc = resample_taps_dev(e, p, &taps)) return rc;
     {
         ProfScope ps(e, AID_K_RESAMPLE, s);
-        launch_resample(src, in_base, n, channels, p.up, p.down, p.hl, p.J, taps, dst, m_first, count, s);
+        launch_resample(src, in_base, n, channels, p.up, p.down, p.hl, p.J, taps, dst, m_first, count, s, n_streams,
+                        src_stride, dst_stride);
     }
     HIP_TRY(hipGetLastError());
     return AID_OK;
@@ -1354,6 +1374,7 @@ static int finalize_locked(aid_engine *e) {
     HIP_TRY(e->idx_off.reserve(K));
     HIP_TRY(e->scan_tmp.reserve(4 * (K / 1024 + 2) + 4096));
     HIP_TRY(e->idx_post.reserve((size_t)std::max<int64_t>(e->n_post, 1)));
+    HIP_TRY(e->idx_sig.reserve((size_t)std::max<int64_t>(e->n_post, 1)));
     if (e->n_tracks == 0) HIP_TRY(e->tomb.reserve(1024));
     HIP_TRY(hipMemsetAsync(e->idx_cnt.p, 0, K * sizeof(uint32_t), s));
     HIP_TRY(e->nz.reserve(1));
@@ -1381,7 +1402,7 @@ static int finalize_locked(aid_engine *e) {
                                             any_removed ? e->tomb.p : nullptr, e->n_tracks,
                                             e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
                                             rocprim_ab, e->srt_scratch.p, e->idx_cnt.p, e->idx_off.p, e->nz.p, &sorted,
-                                            s));
+                                            e->idx_sig.p, s));
             if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended
         }
     } else {
@@ -1391,6 +1412,7 @@ static int finalize_locked(aid_engine *e) {
         HIP_TRY(hipMemcpyAsync(e->idx_cnt.p, e->idx_off.p, K * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         launch_index_scatter(e->p_hash.p, e->p_track.p, e->p_t.p, e->n_post, e->tomb.p, e->n_tracks, e->idx_cnt.p,
                              e->idx_post.p, s);
+        launch_make_sig(e->idx_post.p, e->n_post, e->idx_sig.p, s);  // (only the first n_indexed are read)
     }
     HIP_TRY(hipGetLastError());
     uint32_t total = 0;
@@ -1424,9 +1446,11 @@ int aid_index_finalize(aid_engine *e) {
 int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset) {
     if (!e || (n > 0 && !out)) return fail(AID_ERR_INVALID, "aid_match_stats: bad argument");
     std::lock_guard<std::mutex> lk(e->mu);
-    const int64_t v[6] = {e->st_queries, e->st_votes, e->st_post_reads, e->st_q_lds, e->st_q_global, e->st_records};
-    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
-    if (reset) e->st_queries = e->st_votes = e->st_post_reads = e->st_q_lds = e->st_q_global = e->st_records = 0;
+    const int64_t v[7] = {e->st_queries, e->st_votes,    e->st_post_reads, e->st_q_lds,
+                          e->st_q_global, e->st_records, e->st_sig_reads};
+    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+    if (reset)
+        e->st_queries = e->st_votes = e->st_post_reads = e->st_q_lds = e->st_q_global = e->st_records = e->st_sig_reads = 0;
     return AID_OK;
 }
 
@@ -1715,6 +1739,24 @@ int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t
     return AID_OK;
 }
 
+int aid_index_checksum(aid_engine *e, int64_t first, int64_t count, uint64_t *out) {
+    if (!e || !out || first < 0 || count < 0 || first + count > e->n_post)
+        return fail(AID_ERR_INVALID, "aid_index_checksum: bad range");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    HIP_TRY(e->chk.reserve(1));
+    hipStream_t s = e->own_stream;
+    HIP_TRY(hipMemsetAsync(e->chk.p, 0, sizeof(unsigned long long), s));
+    launch_index_checksum(e->p_hash.p, e->p_track.p, e->p_t.p, first, count, e->chk.p, s);
+    HIP_TRY(hipGetLastError());
+    unsigned long long v = 0;
+    HIP_TRY(hipMemcpyAsync(&v, e->chk.p, sizeof(v), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *out = (uint64_t)v;
+    return AID_OK;
+}
+
 static const char kIdxMagic[8] = {'A', 'I', 'D', 'F', 'P', 'I', 'X', '1'};
 
 int aid_index_save(aid_engine *e, const char *path) {
@@ -1847,7 +1889,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         {
             ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p, s);
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
+                             e->idx_sig.p, s);
         }
         HIP_TRY(hipGetLastError());
         spec_n.resize(nq);
@@ -1875,7 +1918,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         e->st_records += h_count[q];
     }
     if (speculate)  // the LDS path ran every query once: two enumerations (counting, then the exact inserts)
-        for (int q = 0; q < nq; ++q) e->st_post_reads += 2 * h_votes[q];
+        for (int q = 0; q < nq; ++q) e->st_sig_reads += 2 * h_votes[q];
     // global histogram, sized for the votes that pass K5a's 2^20-bit seen filter (all but the
     // distinct bits: v - m(1 - e^{-v/m})) at ~2 per bucket: a chance bucket reaching
     // min_match - 1 then has probability ~1e-5. Sizing it for ALL votes (2 buckets each: 2 MB rows on
@@ -1905,7 +1948,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         {
             ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p, s);
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
+                             e->idx_sig.p, s);
         }
         HIP_TRY(hipGetLastError());
         std::vector<int32_t> got_n(nq);
@@ -1920,7 +1964,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         }
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();
-        for (int q = 0; q < nq; ++q) e->st_post_reads += 2 * h_votes[q];  // counting pass + insert pass
+        for (int q = 0; q < nq; ++q) e->st_sig_reads += 2 * h_votes[q];  // counting pass + insert pass (2 B each)
         e->st_q_lds += nq;
     }
     if (speculate) e->st_q_lds += nq;
@@ -2056,6 +2100,21 @@ int aid_query_pcm(aid_engine *e, const float *pcm, const int64_t *offsets, int32
     if (int rc = ensure_index(e)) return rc;
     if (int rc = extract_locked(e, pcm, offsets, n_clips, loc, stream)) return drain_host_copy(e, loc, stream, rc);
     return drain_host_copy(e, loc, stream, query_extracted_locked(e, rows, nrows));
+}
+
+int aid_query_windows(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends, int32_t n_windows,
+                      aid_match_row *rows, int32_t *nrows, void *stream) {
+    if (!e || n_windows < 0 || (n_windows > 0 && (!starts || !ends || !rows || !nrows)))
+        return fail(AID_ERR_INVALID, "aid_query_windows: bad argument");
+    for (int c = 0; c < n_windows; ++c)
+        if (starts[c] < 0 || ends[c] < starts[c]) return fail(AID_ERR_INVALID, "aid_query_windows: bad window");
+    if (n_windows > 0 && !pcm) return fail(AID_ERR_INVALID, "aid_query_windows: null pcm");
+    if (n_windows == 0) return AID_OK;
+    // one critical section, as aid_query_pcm: K1 reads every window in place (they may overlap), then K5
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = ensure_index(e)) return rc;
+    if (int rc = extract_locked(e, pcm, starts, n_windows, AID_PCM_DEVICE, stream, ends)) return rc;
+    return query_extracted_locked(e, rows, nrows);
 }
 
 }  // extern "C"

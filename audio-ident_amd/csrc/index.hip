@@ -94,6 +94,21 @@ __global__ __launch_bounds__(1024) void k_scan_add(uint32_t *__restrict__ out, c
 
 void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
 
+// K5's 2-B vote signatures of the CSR's postings (aidfp_layout.h posting_sig), for the builds that do not write
+// them in their last pass (the atomic build and the rocPRIM A/B; the radix build fuses it)
+__global__ __launch_bounds__(256) void k_make_sig(const uint64_t *__restrict__ post, int64_t n, uint16_t *__restrict__ sig) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = post[i];
+        sig[i] = posting_sig((uint32_t)v, (uint32_t)(v >> 32));
+    }
+}
+
+void launch_make_sig(const uint64_t *post, int64_t n, uint16_t *sig, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(k_make_sig, dim3((unsigned)blocks), dim3(256), 0, s, post, n, sig);
+}
+
 // ---- posting compaction (aid_index_compact): drop the postings of removed tracks, order kept ----
 // The store's LMDB delete (`olaf_c del`, fingerprint.py:239-246) frees the track's entries; here a
 // removal only tombstones the track, and compaction reclaims its postings. 1024 postings per block.
@@ -199,6 +214,7 @@ struct QueryParams {
     uint32_t *hot;             // [nq][2^hist_bits / 32] bit per histogram bucket >= min_match (K5h)
     int32_t parts;             // K5a workgroups (key partitions) per query
     const int64_t *votes;      // [nq] exact votes per query (k_query_votes, earlier on the stream); LDS path only
+    const uint16_t *sig;       // [n] 2-B vote signature per posting (aidfp_layout.h posting_sig); LDS path only
 };
 
 // Every vote (track, d = t_ref - t_q, t_q) of query records [a, a + n), for the calling wave's
@@ -221,8 +237,8 @@ struct QueryParams {
 #define AID_K5_CHUNK 1  // A/B builds only: 0 = 64-record groups
 #endif
 template <int U, typename G>
-__device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw,
-                                                    int lane, G &&g) {
+__device__ __forceinline__ void for_each_window(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
+                                                G &&g) {
 #if AID_K5_CHUNK
     const int64_t rounds = (n + (int64_t)nw * 64 - 1) / ((int64_t)nw * 64);
     const int64_t chunk = rounds ? (n + nw * rounds - 1) / (nw * rounds) : 64;
@@ -290,19 +306,29 @@ __device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64
                     }
                 }
             }
-            uint64_t e[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) e[u] = qp.post[pos[u]];
-            if (qp.tomb_live) {  // uniform
-                uint8_t tb[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) tb[u] = qp.tomb[(uint32_t)e[u]];
-#pragma unroll
-                for (int u = 0; u < U; ++u) ok[u] = ok[u] && !tb[u];
-            }
-            g(e, tqs, ok);
+            g(pos, tqs, ok);
         }
     }
+}
+
+// for_each_window with each window's postings loaded (and removed tracks' votes dropped while tombstones are newer
+// than the CSR): g(e, tq, ok) for U windows at once
+template <int U, typename G>
+__device__ __forceinline__ void for_each_vote_batch(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw,
+                                                    int lane, G &&g) {
+    for_each_window<U>(qp, a, n, wave, nw, lane, [&](const uint32_t *pos, const int32_t *tqs, bool *ok) {
+        uint64_t e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) e[u] = qp.post[pos[u]];
+        if (qp.tomb_live) {  // uniform
+            uint8_t tb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) tb[u] = qp.tomb[(uint32_t)e[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u) ok[u] = ok[u] && !tb[u];
+        }
+        g(e, tqs, ok);
+    });
 }
 
 template <int U, typename F>
@@ -515,9 +541,6 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 // Phase 4: best d per track, rank, write rows (same as K5b). Any table overflow, or a
 //          16-bit counter reaching 0xFFFF, reports nrows = -1 and the host re-runs the query
 //          on the global-histogram path.
-#ifndef AID_K5_LDS_U
-#define AID_K5_LDS_U 2  // A/B builds only
-#endif
 // 8-bit counters (64 KB) and a 2048-entry exact table: two workgroups per CU, so one query's
 // barriers and table phases overlap another's posting reads. (Four 512-thread workgroups with 2^15 counters and a
 // 1024-entry table ran K5 2.5 % faster on config 4 but sent a bench query to the global path: dropped.) A counter that wraps past 255 marks
@@ -530,7 +553,10 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 #ifndef AID_K5_LDS_THREADS
 #define AID_K5_LDS_THREADS 1024
 #endif
-constexpr int kLdsWindows = AID_K5_LDS_U;  // windows of 64 posting loads a wave keeps in flight (LDS path)
+#ifndef AID_K5_SIG_U
+#define AID_K5_SIG_U 4  // A/B builds only (6 and 8 spill at the 64 VGPRs of 8 waves per SIMD)
+#endif
+constexpr int kLdsSigWindows = AID_K5_SIG_U;  // windows of 64 two-byte signature loads a wave keeps in flight
 #ifndef AID_K5_HBITS
 #define AID_K5_HBITS 16  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
 #endif
@@ -547,6 +573,23 @@ constexpr int kFastVoteCap = AID_K5_VCAP;
 #endif
 constexpr int kFastTrackCap = AID_K5_TCAP;
 constexpr int kFastThreads = AID_K5_LDS_THREADS;
+
+static_assert(kLdsHistBits <= 16, "the LDS filter's buckets come from 16-bit posting signatures");
+
+// every vote's LDS filter bucket, (sig - tq) mod 2^kLdsHistBits, for the calling wave's share of the records:
+// f(bucket) for live votes, U windows of signature loads in flight
+template <typename F>
+__device__ __forceinline__ void for_each_sig(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
+                                             F &&f) {
+    for_each_window<kLdsSigWindows>(qp, a, n, wave, nw, lane, [&](const uint32_t *pos, const int32_t *tqs, bool *ok) {
+        uint16_t sg[kLdsSigWindows];
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u) sg[u] = qp.sig[pos[u]];
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u)
+            if (ok[u]) f((uint32_t)(sg[u] - (uint32_t)tqs[u]) & ((1u << kLdsHistBits) - 1));
+    });
+}
 
 struct FastLds {
     union {
@@ -584,9 +627,16 @@ void k_match_lds(QueryParams qp) {
     // the query's exact vote total (k_query_votes): below the counter maximum no counter can wrap, so only
     // heavier queries pay for returning atomics (the carry check below)
     const bool check_wrap = qp.votes[q] >= (int64_t)kLdsCtrMax;
-    // phase 1
-    for_each_vote<kLdsWindows>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t) {
-        const uint32_t h = mix_td(tr, d) & hmask;
+#ifndef AID_K5_DIAG
+#define AID_K5_DIAG 0  // timing-only builds (wrong rows): 1 = phase 1 without its LDS atomics, 2 = no phase 3, 3 = both
+#endif
+#if AID_K5_DIAG & 1
+    uint32_t diag_x = 0;
+    for_each_sig(qp, a, n, wave, nw, lane, [&](uint32_t h) { diag_x += h; });
+    if (diag_x == 0xFFFFFFFFu) L.overflow = 2;  // keeps the loads
+#else
+    // phase 1: every vote counted from its posting's 2-B signature alone (bucket = sig - tq = H(track) + d)
+    for_each_sig(qp, a, n, wave, nw, lane, [&](uint32_t h) {
         const uint32_t sh = kLdsCtrBits * (h % kLdsCtrPerWord);
         uint32_t *w = &L.u.hist[h / kLdsCtrPerWord];
         if (check_wrap) {
@@ -610,6 +660,7 @@ void k_match_lds(QueryParams qp) {
             atomicAdd(w, 1u << sh);
         }
     });
+#endif
     __syncthreads();
     if (L.overflow) {  // uniform: the global path answers this query
         if (tid == 0) qp.nrows[q] = -1;
@@ -640,13 +691,10 @@ void k_match_lds(QueryParams qp) {
         L.u.t.tbest[i] = 0ull;
     }
     __syncthreads();
-    // phase 3
-    for_each_vote<kLdsWindows>(qp, a, n, wave, nw, lane, [&](uint32_t tr, int32_t d, int32_t tq) {
-        const uint32_t hf = mix_td(tr, d);
-        const uint32_t h = hf & hmask;
-        if (!((L.hot[h >> 5] >> (h & 31)) & 1u)) return;
+    // the exact (track, d) table insert of one hot vote (slot from the full mix of (track, d))
+    auto insert = [&](uint32_t tr, int32_t d, int32_t tq) {
         const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
-        uint32_t s = (hf >> 20) & (kFastVoteCap - 1);
+        uint32_t s = (mix_td(tr, d) >> 20) & (kFastVoteCap - 1);
         int probes = 0;
         for (;;) {
             const unsigned long long old = atomicCAS(&L.u.t.vkey[s], ~0ull, key);
@@ -658,6 +706,31 @@ void k_match_lds(QueryParams qp) {
             }
             if (++probes >= kProbeMax) { L.overflow = 1; break; }
             s = (s + 1) & (kFastVoteCap - 1);
+        }
+    };
+    // phase 3: the signatures again; only a vote whose bucket is hot reads its 8-B posting and enters the table
+    if (!(AID_K5_DIAG & 2))
+    for_each_window<kLdsSigWindows>(qp, a, n, wave, nw, lane, [&](const uint32_t *pos, const int32_t *tqs, bool *ok) {
+        uint16_t sg[kLdsSigWindows];
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u) sg[u] = qp.sig[pos[u]];
+        bool hot[kLdsSigWindows];
+        uint64_t e[kLdsSigWindows];
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u) {
+            const uint32_t h = (uint32_t)(sg[u] - (uint32_t)tqs[u]) & hmask;
+            hot[u] = ok[u] && ((L.hot[h >> 5] >> (h & 31)) & 1u);
+            e[u] = 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u)  // the rare hot votes' postings, all issued before any is used
+            if (hot[u]) e[u] = qp.post[pos[u]];
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u) {
+            if (!hot[u]) continue;
+            const uint32_t tr = (uint32_t)e[u];
+            if (qp.tomb_live && qp.tomb[tr]) continue;  // a removed track's vote (the filter counted it: superset)
+            insert(tr, (int32_t)(e[u] >> 32) - tqs[u], tqs[u]);
         }
     });
     __syncthreads();
@@ -722,10 +795,10 @@ void k_match_lds(QueryParams qp) {
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
                       int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, const int64_t *votes,
-                      hipStream_t s) {
+                      const uint16_t *sig, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
-                   tomb_live, nullptr, 1, votes};
+                   tomb_live, nullptr, 1, votes, sig};
     timed_launch(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
 }
 
@@ -804,6 +877,37 @@ __global__ void k_count_nonzero(const uint32_t *__restrict__ cnt, int64_t n, uns
 
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s) {
     hipLaunchKernelGGL(k_count_nonzero, dim3(2048), dim3(256), 0, s, cnt, n, out);
+}
+
+// Order-sensitive checksum of postings [first, first + n) of the SoA planes: the sum mod 2^64 of
+// mix64((hash << 32 | t) ^ track * C1 ^ i * C2) over positions i relative to `first` (aidfp.catalog.checksum_np is
+// its host mirror). Replicas with equal checksums hold the same postings in the same order (a collision has
+// probability ~2^-64): the catalog ingest compares them across ranks after the exchange.
+__device__ __forceinline__ uint64_t splitmix64_fin(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_index_checksum(const uint32_t *__restrict__ ph, const uint32_t *__restrict__ ptr,
+                                                        const uint32_t *__restrict__ pt, int64_t first, int64_t n,
+                                                        unsigned long long *__restrict__ out) {
+    uint64_t acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = first + i;
+        const uint64_t key = (((uint64_t)ph[j] << 32) | pt[j]) ^ ((uint64_t)ptr[j] * 0x9E3779B97F4A7C15ull) ^
+                             ((uint64_t)i * 0xD6E8FEB86659FD93ull);
+        acc += splitmix64_fin(key);
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+void launch_index_checksum(const uint32_t *ph, const uint32_t *ptr, const uint32_t *pt, int64_t first, int64_t n,
+                           unsigned long long *out, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_index_checksum, dim3((unsigned)blocks), dim3(256), 0, s, ph, ptr, pt, first, n, out);
 }
 
 uint32_t index_keys() { return kKeys; }

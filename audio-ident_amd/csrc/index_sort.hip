@@ -228,7 +228,8 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
                                                                 const uint32_t *__restrict__ offs, int64_t tiles,
                                                                 uint32_t *__restrict__ keys_out,
                                                                 uint64_t *__restrict__ vals_out,
-                                                                uint32_t *__restrict__ E) {
+                                                                uint32_t *__restrict__ E,
+                                                                uint16_t *__restrict__ sig_out) {
     __shared__ uint32_t s_key[kTile];
     __shared__ uint64_t s_val[kTile];
     __shared__ uint32_t cnt[kSortWaves][kDigits];  // running per-wave counters, then cross-wave offsets
@@ -356,7 +357,9 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
                 const bool run_end = i + 1 == m || ((s_key[i + 1] >> shift) & (kDigits - 1)) != d;
                 if (run_end || s_key[i + 1] != k) atomicMax(&E[k + 1], (uint32_t)(dst + 1));
             }
-            __builtin_nontemporal_store(s_val[i], &vals_out[dst]);
+            const uint64_t v = s_val[i];
+            __builtin_nontemporal_store(v, &vals_out[dst]);
+            sig_out[dst] = posting_sig((uint32_t)v, (uint32_t)(v >> 32));  // K5's 2-B vote signature
         } else {
             keys_out[dst] = k;
             vals_out[dst] = s_val[i];
@@ -490,6 +493,8 @@ __global__ void k_sort_keys(const uint32_t *__restrict__ ph, const uint32_t *__r
     }
 }
 
+void launch_make_sig(const uint64_t *post, int64_t n, uint16_t *sig, hipStream_t s);  // index.hip
+
 int64_t radix_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 
 // scratch of the sort build in u32 units: the tile counts, their scan, and the scans' temporaries
@@ -517,7 +522,7 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
                                    uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
                                    uint32_t *scratch, uint32_t *E, uint32_t *offsets, unsigned long long *nz,
-                                   uint64_t **vals_out, hipStream_t s) {
+                                   uint64_t **vals_out, uint16_t *sig, hipStream_t s) {
     *vals_out = vals0;
     const int64_t K = (int64_t)(1u << 26) + 1;
     const int64_t tiles = radix_tiles(n);
@@ -543,30 +548,33 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
             timed_launch(k_radix_count<true, true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
             digit_starts(counts, tiles, offs, stmp, s);
             timed_launch(k_radix_scatter<true, false, true>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
-                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
+                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr,
+                         (uint16_t *)nullptr);
         } else {
             timed_launch(k_radix_count<true, false>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
             digit_starts(counts, tiles, offs, stmp, s);
             timed_launch(k_radix_scatter<true, false, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
-                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr);
+                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr,
+                         (uint16_t *)nullptr);
         }
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
         digit_starts(counts, tiles, offs, stmp, s);
         timed_launch(k_radix_scatter<false, false>, g, b, 0, s, (const uint32_t *)keys1, (const uint64_t *)vals1,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
-                     kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0, (uint32_t *)nullptr);
+                     kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0, (uint32_t *)nullptr, (uint16_t *)nullptr);
         timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys0, (const uint32_t *)nullptr,
                      (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, counts, tiles);
         digit_starts(counts, tiles, offs, stmp, s);
         timed_launch(k_radix_scatter<false, true>, g, b, 0, s, (const uint32_t *)keys0, (const uint64_t *)vals0,
                      (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
-                     2 * kDigitBits, (const uint32_t *)offs, tiles, (uint32_t *)nullptr, vals1, E);
+                     2 * kDigitBits, (const uint32_t *)offs, tiles, (uint32_t *)nullptr, vals1, E, sig);
         *vals_out = vals1;
     }
-    if (n > 0 && sorted_keys) {  // rocPRIM: run ends from its sorted keys
+    if (n > 0 && sorted_keys) {  // rocPRIM: run ends from its sorted keys, the signatures from its values
         const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_run_ends, dim3((unsigned)blocks), dim3(256), 0, s, sorted_keys, n, E, nz);
+        launch_make_sig(*vals_out, n, sig, s);
     }
     // the hand-written sort wrote E in its last pass; its live keys are the nonzero E entries
     scan8<true>(E, offsets, K, stmp, s, sorted_keys ? nullptr : nz);

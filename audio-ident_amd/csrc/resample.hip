@@ -24,9 +24,13 @@ template <bool STEREO, int MODE>
 __global__ __launch_bounds__(kResThreads) void k_resample(const float *__restrict__ src, int64_t in_base, int64_t n,
                                                          int up, int down, int hl, int J,
                                                          const float *__restrict__ taps, float *__restrict__ dst,
-                                                         int64_t m_first, int64_t m_end) {
+                                                         int64_t m_first, int64_t m_end, int64_t src_stride,
+                                                         int64_t dst_stride) {
     // src[0] is stream sample in_base; samples outside [in_base, in_base + n) read as 0.
     // Outputs m_first .. m_end-1 (stream indices) go to dst[m - m_first].
+    // blockIdx.y = stream of a batch: its input at src + y * src_stride, its output at dst + y * dst_stride (floats)
+    src += (int64_t)blockIdx.y * src_stride;
+    dst += (int64_t)blockIdx.y * dst_stride;
     extern __shared__ float smem[];
     const int tid = threadIdx.x;
     // [up][J] tap table first (when it fits), then the input window
@@ -84,7 +88,10 @@ template <bool STEREO>
 __global__ __launch_bounds__(256) void k_resample_phase(const float *__restrict__ src, int64_t in_base, int64_t n,
                                                        int up, int down, int hl, int J,
                                                        const float *__restrict__ taps, float *__restrict__ dst,
-                                                       int64_t m_first, int64_t m_end) {
+                                                       int64_t m_first, int64_t m_end, int64_t src_stride,
+                                                       int64_t dst_stride) {
+    src += (int64_t)blockIdx.y * src_stride;  // stream of a batch (k_resample)
+    dst += (int64_t)blockIdx.y * dst_stride;
     extern __shared__ float sx[];
     const int tid = threadIdx.x;
     const int64_t m0 = m_first + (int64_t)blockIdx.x * up * kResR;
@@ -151,27 +158,32 @@ int64_t resample_lds_floats(int up, int down, int J) {
     return window_floats(up, down, J) + (taps_in_lds(up, J) ? (((int64_t)up * J + 3) & ~3) : 0);
 }
 
+// n_streams > 1: the same output range of n_streams streams in one launch (grid.y = stream), each stream's input
+// src_stride floats after the previous one's and its output dst_stride floats after; bit for bit the outputs of
+// n_streams single launches (same staging, same fma chain per output)
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
-                     const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s) {
-    if (count <= 0) return;
+                     const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s, int n_streams,
+                     int64_t src_stride, int64_t dst_stride) {
+    if (count <= 0 || n_streams <= 0) return;
     if (use_phase(up, down, J)) {
         const int64_t per = (int64_t)up * kResR;
-        const dim3 g((unsigned)((count + per - 1) / per)), b((unsigned)std::min(256, (up + 63) / 64 * 64));
+        const dim3 g((unsigned)((count + per - 1) / per), (unsigned)n_streams), b((unsigned)std::min(256, (up + 63) / 64 * 64));
         const size_t lds = (size_t)resample_lds_floats(up, down, J) * sizeof(float);
         if (channels == 2)
             hipLaunchKernelGGL((k_resample_phase<true>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst,
-                               m_first, m_first + count);
+                               m_first, m_first + count, src_stride, dst_stride);
         else
             hipLaunchKernelGGL((k_resample_phase<false>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst,
-                               m_first, m_first + count);
+                               m_first, m_first + count, src_stride, dst_stride);
         return;
     }
-    const dim3 g((unsigned)((count + kResBlock - 1) / kResBlock)), b(kResThreads);
+    const dim3 g((unsigned)((count + kResBlock - 1) / kResBlock), (unsigned)n_streams), b(kResThreads);
     const size_t lds = (size_t)resample_lds_floats(up, down, J) * sizeof(float);
     const int64_t m_end = m_first + count;
     const int mode = up == 1 ? 2 : taps_in_lds(up, J) ? 1 : 0;
 #define AID_RS_LAUNCH(ST, MD) \
-    hipLaunchKernelGGL((k_resample<ST, MD>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst, m_first, m_end)
+    hipLaunchKernelGGL((k_resample<ST, MD>), g, b, lds, s, src, in_base, n, up, down, hl, J, taps, dst, m_first, m_end, \
+                       src_stride, dst_stride)
     if (channels == 2) {
         if (mode == 2) AID_RS_LAUNCH(true, 2); else if (mode == 1) AID_RS_LAUNCH(true, 1); else AID_RS_LAUNCH(true, 0);
     } else {

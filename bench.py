@@ -426,6 +426,17 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
             per_rank = [int(st.postings_local)]
         ingest, te, tx, tb, ti, tsyn = ph
         stats = eng.index_stats()
+        # the replicas checked after the timing: checksums compared across ranks, and on rank 0 every rank's
+        # shard against the oracle (a rank-local checker: it reports, it does not raise)
+        from aidfp.catalog import replica_check
+
+        replicas = replica_check(eng)
+        sp = None
+        if rank == 0 and args.shard_parity_tracks > 0:
+            try:
+                sp = shard_parity(eng, tracks, args.catalog_seconds, world, torch, args.shard_parity_tracks)
+            except Exception as exc:
+                sp = {"bit_exact": False, "error": f"{type(exc).__name__}: {exc}"}
         audio = args.catalog_tracks * args.catalog_seconds
         gathered = 12 * sum(per_rank)  # bytes of (hash, track, t) every rank receives
         exact = None
@@ -444,7 +455,8 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
                 "allgather_bytes_per_rank": gathered,
                 "allgather_gbs_per_rank": round(gathered / tx / 1e9, 1) if world > 1 and tx > 0 else None,
                 "union_equals_sum_of_shards": int(st.postings_total) == sum(per_rank),
-                "exact_lane": exact}
+                "replicas_identical": replicas["replicas_identical"], "replica_checksums": replicas,
+                "shard_parity": sp, "exact_lane": exact}
     finally:
         eng.close()
 
@@ -508,7 +520,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     # second (insert) pass and the global path's per-partition re-reads are the implementation's, not the
     # algorithm's: they are reported as issued_bytes, and the bytes that reach HBM come from the PMC passes
     alg = 8 * ms["votes"] + 8 * ms["records"]
-    issued = 8 * ms["posting_reads"] + 8 * ms["records"]
+    issued = 8 * ms["posting_reads"] + 2 * ms.get("sig_reads", 0) + 8 * ms["records"]
     pmc_k5, pmc_src = load_pmc_k5()
     roof = {"kernels": list(K5_KERNELS), "bound": "hbm", "unit": "GB/s", "peak": PEAK,
             "algorithmic_bytes": alg, "issued_bytes": issued, "k5_seconds": round(k5_s, 4),
@@ -519,7 +531,8 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
             "pmc": pmc_k5, "pmc_source": pmc_src,
             "source": "rank 0, untimed second pass of the same clips with HIP events on the K5 kernels",
             "note": "algorithmic bytes = 8 B x votes (one posting read per vote) + 8 B x query records; issued bytes "
-                    "count the LDS path's two enumerations (counting, insert) and the global path's re-reads; the "
+                    "count what the kernels read: the LDS path's two enumerations of 2-B posting signatures (counting, "
+                    "insert; the 8-B postings of hot votes are not counted), the global path's 8-B re-reads; the "
                     "vote filters and exact tables stay in LDS / the caches and are not counted; pmc = the K5 "
                     "kernels' HBM bytes per config-4 lane call (2 x FETCH_SIZE + WRITE_SIZE) from the newest "
                     "committed K5 PMC summary"}
@@ -531,15 +544,12 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
             "parity": par, "path": "aid_exact_lane, 4096 clips per call, 3 sub-windows each"}
 
 
-def _oracle_subset(eng, hashes: np.ndarray, torch, chunk: int = 1 << 26) -> np.ndarray:
-    """The index's stored postings whose hash is one of `hashes`, as a host [m, 3] uint32 (hash, track, t) array
-    sorted for fp_query. The planes are exported to the device chunk by chunk (aid_index_export) and filtered
-    there (a sorted-table lookup per posting), so only the few postings the sampled queries can vote through
-    reach the host. Exact for voting: a query touches only postings whose hash equals one of its records'."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle as O  # checker only
-
-    q = torch.from_numpy(np.unique(hashes.astype(np.uint32)).view(np.int32).copy()).cuda()
+def _postings_where(eng, values: np.ndarray, torch, column: int = 0, chunk: int = 1 << 26) -> np.ndarray:
+    """The index's stored postings whose `column` (0 hash, 1 track, 2 t) is one of `values`, as a host [m, 3]
+    uint32 (hash, track, t) array in storage order. The planes are exported to the device chunk by chunk
+    (aid_index_export) and filtered there (a sorted-table lookup per posting), so only the matching postings
+    reach the host."""
+    q = torch.from_numpy(np.unique(np.asarray(values, dtype=np.uint32)).view(np.int32).copy()).cuda()
     q, _ = torch.sort(q)  # int32 order of the uint32 bits: the same order on both sides of the lookup
     total = eng.index_stats()["postings"]
     n = min(chunk, max(total, 1))
@@ -548,14 +558,58 @@ def _oracle_subset(eng, hashes: np.ndarray, torch, chunk: int = 1 << 26) -> np.n
     for o in range(0, total, chunk):
         c = min(chunk, total - o)
         eng.index_export_device(*(p.data_ptr() for p in planes), o, c)
-        h = planes[0][:c]
+        h = planes[column][:c]
         i = torch.searchsorted(q, h).clamp_(max=len(q) - 1)
         m = q[i] == h
         parts.append(torch.stack([p[:c][m] for p in planes], dim=1).cpu().numpy().view(np.uint32))
     del planes
-    sub = np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros((0, 3), np.uint32))
+    return np.ascontiguousarray(np.concatenate(parts) if parts else np.zeros((0, 3), np.uint32))
+
+
+def _oracle_subset(eng, hashes: np.ndarray, torch) -> np.ndarray:
+    """The index's stored postings whose hash is one of `hashes`, sorted for fp_query: only the postings the
+    sampled queries can vote through reach the host. Exact for voting: a query touches only postings whose hash
+    equals one of its records'."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # checker only
+
+    sub = _postings_where(eng, hashes, torch, column=0)
     O.lib().fp_index_sort(O._ptr(sub), len(sub))
     return sub
+
+
+def shard_parity(eng, tracks: np.ndarray, seconds: float, world: int, torch, per_rank: int = 8) -> dict:
+    """Rank 0, after the exchange: `per_rank` tracks of every rank's shard, synthesised on
+    the host (aidfp.synth, bit-identical to the device generator) and fingerprinted by oracle/fp_oracle.c, must
+    appear in this replica exactly as the postings (hash, track, t) the oracle's records give -- the shards that
+    crossed the exchange (RCCL under the driver's N > 1 runs) arrived intact. Checker only, after the timing."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from aidfp import synth
+    from aidfp.catalog import shard
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # checker only
+
+    t0 = time.perf_counter()
+    n = int(round(seconds * SR)) & ~1
+    picks = []
+    for r in range(world):
+        sh = np.asarray(shard(tracks, r, world))
+        if len(sh):
+            picks += [int(x) for x in np.unique(sh[np.linspace(0, len(sh) - 1, min(per_rank, len(sh))).astype(int)])]
+    with ThreadPoolExecutor(max(1, min(16, cpu_info()["cores"]))) as pool:
+        recs = list(pool.map(lambda t: O.fingerprint(synth.synth(t, 0, n, SR), 512), picks))
+    got = _postings_where(eng, np.array(picks, np.uint32), torch, column=1)
+    bad = []
+    for t, r in zip(picks, recs):
+        mine = got[got[:, 1] == t]
+        a = np.sort((mine[:, 0].astype(np.uint64)) | (mine[:, 2].astype(np.uint64) << np.uint64(32)))
+        if not np.array_equal(a, np.sort(r)):
+            bad.append(t)
+    return {"tracks_checked": len(picks), "ranks": world, "postings_checked": int(sum(len(r) for r in recs)),
+            "bit_exact": not bad, "mismatched_tracks": bad[:8], "seconds": round(time.perf_counter() - t0, 2),
+            "oracle": "aidfp.synth (host) + oracle/fp_oracle.c records vs this replica's postings of those tracks"}
 
 
 def lane_parity(eng, truth, starts, n_pos: int, sel, kept: dict, cat, torch) -> dict:
@@ -664,6 +718,153 @@ def lane_parity(eng, truth, starts, n_pos: int, sel, kept: dict, cat, torch) -> 
             "subset_seconds": round(t_sub, 2),
             "oracle": "oracle/fp_oracle.c records, oracle/fp_match.c fp_query over the index postings with the "
                       "windows' hashes, aidfp.exact.run_exact_lane (per-window path) for the consensus"}
+
+
+def stream_leg(args, rank, world, dist, torch) -> dict:
+    """BASELINE config 5 at serving scale: args.stream_count live 48 kHz stereo streams (browser capture,
+    AudioRecorder.svelte:86-106) identified continuously against a 16 kHz index of args.stream_tracks x 30 s tracks
+    ingested from 44.1 kHz sources through K6 (ffmpeg -ar 16000 of decode.py:41-60). Each stream is a sequence of
+    30 s catalog segments, independent noise per channel at SNR 30 dB. Every push hands 2.5 s (one window hop) of
+    every stream to aidfp.stream.StreamBank: ONE K6 launch (downmix + 48k -> 16k for all streams) and ONE
+    aid_query_windows call (K1-K3 in place over the windows the push completed, then K5). The streams' PCM is
+    generated in HBM before the timed region (a push copies its chunk into the bank's history like a network
+    receive buffer would); value = stream-seconds of all streams / the pushes' wall time. Latency = per push, the
+    call to the rows on the host. top-1 over windows that lie inside one segment. Every rank serves its own
+    streams against its own replica (streams are independent)."""
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.engine import Engine
+    from aidfp.stream import StreamBank
+
+    SSR, QSR = 16000, 48000
+    S, T = args.stream_count, args.stream_tracks
+    seg_s = 30.0
+    n_seg = max(1, int(round(args.stream_seconds / seg_s)))
+    chunk = int(args.stream_chunk_s * QSR)
+    seg = int(seg_s * QSR)
+    eng = Engine(SSR, device=torch.cuda.current_device())
+    out: dict = {}
+    try:
+        def build():
+            t = time.perf_counter()
+            st = ingest_synthetic(eng, np.arange(T, dtype=np.uint32), 30.0, batch=1024, source_sr=44100, local=True)
+            torch.cuda.synchronize()
+            out["index"] = {"tracks": T, "track_seconds": 30.0, "source_sr": 44100, "index_sr": SSR,
+                            "postings": int(st.postings_total), "build_s": round(time.perf_counter() - t, 3)}
+            rng = np.random.default_rng(500 + rank)
+            seg_tracks = rng.integers(0, T, (S, n_seg)).astype(np.uint32)
+            stereo = torch.empty(S, n_seg * seg, 2, dtype=torch.float32, device="cuda")
+            tmp = torch.empty(S * n_seg * seg, dtype=torch.float32, device="cuda")
+            from aidfp import synth
+
+            noise = synth.noise_halfwidth(30.0)
+            for ch in range(2):  # each segment from its track's start, independent noise per channel
+                eng.synth(tmp.data_ptr(), seg_tracks.ravel(), np.zeros(S * n_seg, np.int64), seg, noise_a=noise,
+                          salt=11 + ch, sample_rate=QSR)
+                stereo[:, :, ch] = tmp.view(S, n_seg * seg)
+            del tmp
+            torch.cuda.synchronize()
+            return seg_tracks, stereo
+
+        seg_tracks, stereo = _agreed(build, "stream (index + streams)", dist)
+        total_n = stereo.shape[1]
+
+        def run(n_streams, measure: bool):
+            bank = StreamBank(eng, n_streams, stream_sr=QSR)
+            bank.timings = []
+            eng.match_stats(reset=True)
+            lat, res = [], [[] for _ in range(n_streams)]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for a in range(0, total_n, chunk):
+                t = time.perf_counter()
+                r = bank.push(stereo[:n_streams, a:a + chunk])
+                lat.append(time.perf_counter() - t)
+                for i in range(n_streams):
+                    res[i] += r[i]
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0, lat, res, bank.timings, eng.match_stats(reset=True)
+
+        def local():
+            run(S, False)  # warm-up: first-use allocations of the bank and the engine's scratch
+            return run(S, True)
+
+        wall, lat, res, tim, mst = _agreed(local, "stream (pushes)", dist)
+        worst = int(np.argmax(lat))
+        out["slowest_push"] = {"index": worst, "ms": round(1e3 * lat[worst], 3),
+                               "append_resample_windows_ms": [round(1e3 * x, 3) for x in tim[worst]]}
+        out["match_stats"] = mst
+        wall_max = _max_over_ranks(wall, dist, torch)
+        hits = inside = windows = 0
+        for i in range(S):
+            for r in res[i]:
+                windows += 1
+                a, b = r.start_s, r.start_s + 5.0
+                j = int(a // seg_s)
+                if j == int((b - 1e-9) // seg_s):
+                    inside += 1
+                    hits += r.best_track == int(seg_tracks[i, j])
+        lat_ms = 1e3 * np.array(lat)
+        stream_s = S * total_n / QSR
+        out.update({
+            "value": round(world * stream_s / wall_max, 1), "unit": "stream-audio-s/s", "streams_per_rank": S,
+            "stream_seconds": total_n / QSR, "pushes": len(lat), "chunk_s": args.stream_chunk_s,
+            "windows_per_rank": windows, "wall_s_max_over_ranks": round(wall_max, 4),
+            "push_latency_ms": {**{f"p{q}": round(float(np.percentile(lat_ms, q)), 3) for q in (50, 95, 99)},
+                                "max": round(float(lat_ms.max()), 3), "all": [round(float(x), 3) for x in lat_ms]},
+            "realtime_factor_per_gpu": round(stream_s / wall_max, 1),
+            "top1_inside_segments": round(hits / max(1, inside), 4), "windows_inside_segments": inside,
+            "path": "aidfp.stream.StreamBank: per push one aid_resample_batch (48 kHz stereo -> 16 kHz mono, all "
+                    "streams) + one aid_query_windows (K1-K3 in place over every completed 5 s / 2.5 s-hop window, K5)",
+            "data": "synthetic 30 s catalog segments at 48 kHz, SNR 30 dB per channel, generated in HBM"})
+        if rank == 0 and args.stream_parity_streams > 0:
+            try:
+                out["parity"] = stream_parity(eng, stereo, seg_tracks, res, args.stream_parity_streams, torch)
+            except Exception as exc:
+                out["parity"] = {"bit_exact": False, "error": f"{type(exc).__name__}: {exc}"}
+        del stereo
+    finally:
+        eng.close()
+    return out
+
+
+def stream_parity(eng, stereo, seg_tracks, res, n_streams: int, torch, max_windows: int = 8) -> dict:
+    """The first `n_streams` streams' first windows against the oracle route (checker only, after the timing): the
+    host downmix (L + R) * 0.5f and oracle/fp_resample.c's 48k -> 16k (FPSPEC 8), each window fingerprinted by
+    oracle/fp_oracle.c and matched by oracle/fp_match.c fp_query over this index's postings with its hashes; the
+    rows must equal the ones StreamBank returned."""
+    import ctypes
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # checker only
+
+    t0 = time.perf_counter()
+    QSR, SSR = 48000, eng.sample_rate
+    win, hop = int(round(5.0 * SSR)) & ~1, int(round(2.5 * SSR)) & ~1
+    nw = min(max_windows, len(res[0]))
+    need = ((nw - 1) * hop + win) * QSR // SSR + 4096  # stream frames the first nw windows (and their filter) read
+    recs, want = [], []
+    for i in range(n_streams):
+        x = stereo[i, :min(need, stereo.shape[1])].cpu().numpy()
+        mono = ((x[:, 0] + x[:, 1]) * np.float32(0.5)).astype(np.float32)
+        y = O.resample(mono, QSR, SSR)
+        for j in range(nw):
+            s0 = int(round(res[i][j].start_s * SSR))
+            recs.append(O.fingerprint(y[s0:s0 + win], eng.hop))
+            want.append(res[i][j].rows)
+    sub = _oracle_subset(eng, np.concatenate([r & np.uint64(0xFFFFFFFF) for r in recs]), torch)
+    bad = []
+    for k, r in enumerate(recs):
+        qh = np.ascontiguousarray((r & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+        qt = np.ascontiguousarray((r >> np.uint64(32)).astype(np.uint32))
+        rows = (O.Row * eng.max_results)()
+        m = int(O.lib().fp_query(O._ptr(sub), len(sub), O._ptr(qh), O._ptr(qt), len(r), eng.min_match,
+                                 ctypes.addressof(rows), eng.max_results))
+        got = np.array([[x.match_count, x.track, x.d, x.tq_min, x.tq_max] for x in rows[:m]], np.int64).reshape(-1, 5)
+        if not np.array_equal(got, want[k]):
+            bad.append(k)
+    return {"streams": n_streams, "windows": len(recs), "bit_exact": not bad, "mismatched_windows": bad[:8],
+            "seconds": round(time.perf_counter() - t0, 2),
+            "oracle": "host downmix + oracle/fp_resample.c + oracle/fp_oracle.c + oracle/fp_match.c fp_query"}
 
 
 def service_leg(args, rank, world, dist, torch) -> dict:
@@ -791,8 +992,17 @@ def main() -> int:
     ap.add_argument("--exact-clips", type=int, default=10000,
                     help="config-4 positive query clips per rank against the catalog leg's index, plus 10 %% "
                          "negatives from unseen tracks (BASELINE configs[3]: 10k; 0 = skip)")
+    ap.add_argument("--shard-parity-tracks", type=int, default=8,
+                    help="tracks of every rank's shard rank 0 checks against the oracle after the exchange (0 = none)")
     ap.add_argument("--lane-parity-clips", type=int, default=64,
                     help="exact-lane clips per rank checked against the oracle at the catalog's scale (0 = none)")
+    ap.add_argument("--no-stream", action="store_true", help="skip the config-5 multi-stream leg")
+    ap.add_argument("--stream-count", type=int, default=256, help="live 48 kHz stereo streams per rank (config 5)")
+    ap.add_argument("--stream-tracks", type=int, default=10000, help="tracks of the stream leg's 16 kHz index")
+    ap.add_argument("--stream-seconds", type=float, default=60.0, help="length of every stream (30 s segments)")
+    ap.add_argument("--stream-chunk-s", type=float, default=2.5, help="seconds of every stream per push")
+    ap.add_argument("--stream-parity-streams", type=int, default=2,
+                    help="streams whose first windows rank 0 checks against the oracle route (0 = none)")
     ap.add_argument("--no-service", action="store_true", help="skip the drop-in service leg")
     ap.add_argument("--service-tracks", type=int, default=10000)
     ap.add_argument("--service-requests", type=int, default=512)
@@ -955,7 +1165,7 @@ def main() -> int:
     # The extra legs (catalog ingest with its RCCL exchange, exact lane, service) run after the headline is measured.
     # A leg that never returns (a collective stuck on some rank) must not cost the headline line: past the deadline a
     # watchdog prints the line with the unfinished legs marked and ends the process (every rank runs the same timer)
-    legs = {"catalog": None, "service": None}
+    legs = {"catalog": None, "service": None, "stream": None}
     stage = ["catalog"]  # the leg running now, for the watchdog's report
     emitted = threading.Lock()
     finished = threading.Event()
@@ -964,7 +1174,7 @@ def main() -> int:
         if not emitted.acquire(blocking=False):
             return False
         if rank == 0:
-            print(json.dumps(make_line(legs["catalog"], legs["service"])), flush=True)
+            print(json.dumps(make_line(legs["catalog"], legs["service"], legs["stream"])), flush=True)
         return True
 
     def watchdog():
@@ -989,14 +1199,21 @@ def main() -> int:
         return ok
 
     def ok_lane() -> bool:
-        """The config-4 lane's parity at the catalog's scale (catalog.exact_lane.parity), when it ran."""
-        lane = (legs["catalog"] or {}).get("exact_lane") or {}
-        lp = lane.get("parity")
+        """The catalog's own checks, when they ran: the config-4 lane's parity at the catalog's scale
+        (catalog.exact_lane.parity), identical replicas on every rank and the shards' postings against the oracle."""
+        cat = legs["catalog"] or {}
+        if cat.get("replicas_identical") is False:
+            return False
+        if (cat.get("shard_parity") or {}).get("bit_exact") is False:
+            return False
+        if ((legs["stream"] or {}).get("parity") or {}).get("bit_exact") is False:
+            return False
+        lp = (cat.get("exact_lane") or {}).get("parity")
         if not lp:
             return True
         return bool(lp.get("records_bit_exact") and lp.get("rows_bit_exact") and lp.get("lane_equal"))
 
-    def make_line(catalog, service) -> dict:
+    def make_line(catalog, service, stream) -> dict:
         return {
             "metric": METRIC,
             "value": round(value, 1),
@@ -1028,11 +1245,12 @@ def main() -> int:
             "fullband": fullband,
             "catalog": catalog,
             "service": service,
+            "stream": stream,
             "cpu_baseline": cpu,
             "parity": par,
         }
 
-    if args.leg_deadline > 0 and not (args.no_catalog and args.no_service):
+    if args.leg_deadline > 0 and not (args.no_catalog and args.no_service and args.no_stream):
         threading.Thread(target=watchdog, daemon=True).start()
     catalog = None
     if not args.no_catalog:
@@ -1053,6 +1271,15 @@ def main() -> int:
         legs["service"] = service
 
     _log("service done")
+    stage[0] = "stream"
+    stream = None
+    if not args.no_stream:
+        try:  # stream_leg agrees on its rank-local parts, so every rank takes this branch alike
+            stream = stream_leg(args, rank, world, dist, torch)
+        except Exception as exc:  # the headline stands on its own
+            stream = {"error": f"{type(exc).__name__}: {exc}"}
+        legs["stream"] = stream
+    _log("stream done")
     if os.environ.get("AIDFP_DUMP_MAPS"):  # diagnostics: the process's mappings, to symbolise an exit-time trace
         Path(os.environ["AIDFP_DUMP_MAPS"]).write_text(Path("/proc/self/maps").read_text())
     finished.set()
@@ -1061,7 +1288,7 @@ def main() -> int:
     if dist:
         dist.destroy_process_group()
     if not ok_lane():
-        _log("exact-lane parity at the catalog's scale FAILED (catalog.exact_lane.parity)")
+        _log("catalog checks FAILED (catalog.replicas_identical, catalog.shard_parity or catalog.exact_lane.parity)")
     return 0 if ok_headline() and ok_lane() else 1
 
 

@@ -192,16 +192,22 @@ int aid_index_remove(aid_engine *e, uint32_t track);
  * `olaf_c del` frees its entries). *n_removed = postings dropped. The CSR is rebuilt lazily. */
 int aid_index_compact(aid_engine *e, int64_t *n_removed);
 int aid_index_finalize(aid_engine *e);
-/* Cumulative match counters since the last reset: out[0] queries, [1] exact votes (postings whose hash
-   a query record hits), [2] postings K5 read (LDS path: twice per vote, its counting and insert passes;
-   global path: once per key partition in K5a + once in K5b), [3] queries answered on the LDS path, [4] on the global path,
-   [5] query records. The match roofline is 8 B x out[2] / the K5 kernels' time. */
+/* Cumulative match counters since the last reset (the first n of 7): out[0] queries, [1] exact votes (postings whose
+   hash a query record hits), [2] 8-B postings K5's global path read (once per key partition in K5a + once in K5b),
+   [3] queries answered on the LDS path, [4] on the global path, [5] query records, [6] 2-B posting signatures the
+   LDS path read (twice per vote: its counting and insert passes; the insert pass also reads the 8-B posting of a
+   vote whose bucket is hot). */
 int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset);
 /* n_postings = stored postings, n_live = postings in the built CSR (-1 if stale), n_tracks = max id + 1 */
 int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks);
 /* Copy stored postings [first, first+count) to host or device columns (RCCL all-gather export). */
 int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t, int64_t first, int64_t count,
                      int32_t location);
+/* Order-sensitive 64-bit checksum of stored postings [first, first+count), computed on the device:
+   sum mod 2^64 over i of splitmix64-finalizer((hash << 32 | t) ^ track * 0x9E3779B97F4A7C15 ^ i * 0xD6E8FEB86659FD93),
+   i counted from `first`. After the catalog exchange every rank compares its replica's checksum with the others'
+   (the sequential ingest it replaces, app/ingest/pipeline.py:294-310, had one LMDB and nothing to compare). */
+int aid_index_checksum(aid_engine *e, int64_t first, int64_t count, uint64_t *out);
 /* ---- PCM front-end (spec/FPSPEC.md 8) ----
  * Replaces ffmpeg `-ac 1 -ar <rate>` (audio-ident-service/app/audio/decode.py:41-60): optional
  * stereo downmix ((L+R)*0.5f) + rational polyphase resampling sr_in -> sr_out (scipy
@@ -217,6 +223,13 @@ int aid_resample(aid_engine *e, const float *src, int64_t n, int32_t channels, i
  * whole-signal result chunk by chunk (aidfp.stream). */
 int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t n, int32_t channels, int32_t sr_in,
                        int32_t sr_out, int64_t m_first, int64_t count, float *dst, void *stream);
+/* aid_resample_range for n_streams streams in lockstep, ONE launch (config 5: every stream of a bank pushes
+ * the same chunk length): stream i's input starts src_stride floats after stream i-1's, its outputs
+ * dst_stride floats after. Each stream's outputs are bit for bit those of its own aid_resample_range.
+ * Replaces one ffmpeg `-ac 1 -ar` process per upload (decode.py:41-60) for a whole batch of live streams. */
+int aid_resample_batch(aid_engine *e, const float *src, int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n,
+                       int32_t channels, int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
+                       int64_t dst_stride, void *stream);
 /* (up, down, hl, J) of a rate pair (FPSPEC 8); returns 0 on bad rates */
 int aid_resample_plan(int32_t sr_in, int32_t sr_out, int32_t *up, int32_t *down, int32_t *hl, int32_t *J);
 
@@ -289,6 +302,11 @@ int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows);
    fingerprint.py:185-193). Synchronous. */
 int aid_query_pcm(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t pcm_location,
                   aid_match_row *rows, int32_t *nrows, void *stream);
+/* aid_query_pcm over windows of DEVICE PCM given as [starts[c], ends[c]) sample ranges, which may overlap
+ * (50 %-overlap stream windows, sub-windows of one clip): K1-K3 read them in place, then K5, in one critical
+ * section. Rows as aid_query. Replaces one `olaf_c query` per window (fingerprint.py:185-193). */
+int aid_query_windows(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends, int32_t n_windows,
+                      aid_match_row *rows, int32_t *nrows, void *stream);
 
 /* Batched exact lane: replaces app/search/exact.py run_exact_lane's
    sub-window fan-out, the olaf_query calls and the consensus (exact.py:70-124, :132-353) for a

@@ -80,7 +80,7 @@ def main():
         out[name] = {"s": [round(x, 4) for x in ts], "clips_per_s": round(n / min(ts), 1), "top1": top1,
                      "rows_equal_auto": same, "votes_per_query": round(ms["votes"] / max(1, ms["queries"]), 1),
                      "queries_lds": ms["queries_lds"], "queries_global": ms["queries_global"],
-                     "k5_ms": round(k5_ms, 3), "k5_frac": round(8 * ms["posting_reads"] / reps_or1(args) / k5_ms / 8e9, 4) if k5_ms else None}
+                     "k5_ms": round(k5_ms, 3), "k5_frac": round(8 * ms["votes"] / reps_or1(args) / k5_ms / 8e9, 4) if k5_ms else None}
         print(json.dumps({name: out[name]}), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 

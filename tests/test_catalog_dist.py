@@ -56,6 +56,14 @@ class HostEngine:
             v[q * stride: q * stride + n] = self.post[first:, q]
             v[q * stride + n: (q + 1) * stride] = 0
 
+    def index_checksum(self, first=0, count=None):  # aid_index_checksum stand-in: its host mirror
+        from aidfp.catalog import checksum_np
+
+        return checksum_np(self.post[first:] if count is None else self.post[first:first + count])
+
+    def index_stats(self):
+        return {"postings": len(self.post), "live": len(self.post), "tracks": self.n_tracks}
+
     def index_splice(self, first, ptr, counts, stride, n_tracks):
         parts = [self.post[:first]]
         if stride:
@@ -220,3 +228,60 @@ def test_shard_balanced_and_complete():
         parts = [shard(tracks, r, world) for r in range(world)]
         assert np.array_equal(np.concatenate(parts), tracks)
         assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+def _replica_worker(rank, world, port, q, corrupt_rank):
+    """Exchange, then the replica check every bench line carries (catalog.replicas_identical): equal everywhere,
+    unless one rank's replica is altered after the exchange."""
+    from aidfp.catalog import replica_check
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = _blocks(world)[rank]
+        eng = HostEngine(np.concatenate([KEEP, mine]), n_tracks=100 * rank + len(mine))
+        exchange_postings(eng, first=len(KEEP))
+        if rank == corrupt_rank:
+            eng.post = eng.post.copy()
+            eng.post[[2, 3]] = eng.post[[3, 2]]  # same postings, two swapped: order matters
+        q.put((rank, replica_check(eng)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,corrupt", [(2, -1), (3, -1), (3, 2)])
+def test_replica_check_gloo(world, corrupt):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, world, port, q, corrupt)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=120) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(world):
+        assert res[r]["ranks"] == world
+        assert res[r]["replicas_identical"] == (corrupt < 0)
+        assert res[r]["mismatched_ranks"] == ([] if corrupt < 0 else [corrupt])
+
+
+def test_checksum_mirror_properties():
+    """aid_index_checksum's host mirror: order-sensitive, position-relative, sensitive to every column."""
+    from aidfp.catalog import checksum_np
+
+    rng = np.random.default_rng(1)
+    p = rng.integers(0, 2**32, size=(1000, 3), dtype=np.uint64).astype(np.uint32)
+    c = checksum_np(p)
+    assert c == checksum_np(p.copy()) and 0 <= c < 2**64
+    assert checksum_np(p[::-1]) != c
+    for col in range(3):
+        q = p.copy()
+        q[500, col] ^= 1
+        assert checksum_np(q) != c
+    # a range's checksum counts positions from its own start
+    assert checksum_np(p[10:]) == checksum_np(p[10:], 0) != checksum_np(p[10:], 10)
+    assert checksum_np(np.zeros((0, 3), np.uint32)) == 0

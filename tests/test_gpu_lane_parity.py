@@ -54,3 +54,25 @@ def test_lane_parity_small_catalog(catalog, category):
     assert par["k5_paths"]["lds"]["queries_lds"] == par["windows"]
     # the positives were found (the check is not vacuous)
     assert sum(len(kept[int(q)]) > 0 for q in sel if q < n_pos) >= 5
+
+
+def test_index_checksum_equals_host_mirror(catalog):
+    """aid_index_checksum (device) equals its host mirror over the exported postings, whole and by range."""
+    from aidfp.catalog import checksum_np
+
+    eng = catalog
+    post = eng.index_export()
+    assert eng.index_checksum() == checksum_np(post)
+    n = len(post)
+    assert eng.index_checksum(n // 3, n // 2) == checksum_np(post[n // 3: n // 3 + n // 2])
+    assert eng.index_checksum(n, 0) == 0
+
+
+def test_shard_parity_small_catalog(catalog):
+    """bench.shard_parity: the oracle's fingerprints of sampled tracks of every (pretend) rank's shard equal this
+    index's postings of those tracks."""
+    import torch
+
+    par = bench.shard_parity(catalog, np.arange(N_TRACKS, dtype=np.uint32), 30.0, 3, torch, per_rank=4)
+    assert par["bit_exact"], par
+    assert par["tracks_checked"] == 12 and par["postings_checked"] > 1000

@@ -44,3 +44,70 @@ def test_stream_windows_identify_segments():
             s0 = int(round(r.start_s * SR))
             if s0 // seg == (s0 + sid.win - 1) // seg:
                 assert r.best_track == order[s0 // seg]
+
+
+def _stereo_streams(tracks_per_stream, seg_s, sr, salt0=0):
+    seg = int(seg_s * sr)
+    out = []
+    for i, order in enumerate(tracks_per_stream):
+        L = np.concatenate([synth.synth(int(t), 0, seg, sr, snr_db=30.0, salt=salt0 + 2 * i + 1) for t in order])
+        R = np.concatenate([synth.synth(int(t), 0, seg, sr, snr_db=30.0, salt=salt0 + 2 * i + 2) for t in order])
+        out.append(np.stack([L, R], axis=1))
+    return np.stack(out)  # [S, n, 2]
+
+
+@pytest.mark.parametrize("device_chunks", [True, False])
+def test_stream_bank_equals_single_streams(device_chunks):
+    """StreamBank (one K6 launch + one aid_query_windows call per push for all streams) gives every stream exactly
+    the windows and rows of its own StreamIdentifier (per-stream K6 + per-stream queries), with buffer compaction
+    and chunks that are not a multiple of the hop."""
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.stream import StreamBank
+
+    with Engine(16000) as eng:
+        ingest_synthetic(eng, np.arange(30, dtype=np.uint32), 30.0, source_sr=44100)
+        orders = [[3, 17], [29, 4], [11, 11], [0, 25], [7, 8]]
+        st = _stereo_streams(orders, 12.0, SR)  # 24 s per stream
+        bank = StreamBank(eng, len(orders), stream_sr=SR, capacity_s=12.0)  # forces compaction of both buffers
+        singles = [StreamIdentifier(eng, capacity_s=12.0, stream_sr=SR) for _ in orders]
+        step = 50000
+        got = [[] for _ in orders]
+        want = [[] for _ in orders]
+        for a in range(0, st.shape[1], step):
+            chunk = st[:, a:a + step]
+            res = bank.push(torch.from_numpy(np.ascontiguousarray(chunk)).cuda() if device_chunks else chunk)
+            for i in range(len(orders)):
+                got[i] += res[i]
+                want[i] += singles[i].push(chunk[i])
+        for i in range(len(orders)):
+            assert len(got[i]) == len(want[i]) == int((st.shape[1] / SR - 5.0) // 2.5) + 1
+            for g, w in zip(got[i], want[i]):
+                assert g.start_s == w.start_s and np.array_equal(g.rows, w.rows), (i, g.start_s)
+        # and the windows inside a 12 s segment name its track
+        hits = total = 0
+        for i, order in enumerate(orders):
+            for r in got[i]:
+                a, b = r.start_s, r.start_s + 5.0
+                if int(a // 12.0) == int((b - 1e-9) // 12.0):
+                    total += 1
+                    hits += r.best_track == order[int(a // 12.0)]
+        assert total >= 10 and hits == total
+
+
+def test_resample_batch_equals_single_streams(gpu_engine):
+    """aid_resample_batch: n streams in one launch = n aid_resample_range calls, bit for bit (48k -> 16k and
+    48k -> 44.1k stereo, 44.1k -> 16k mono)."""
+    rng = np.random.default_rng(4)
+    for sr_in, sr_out, ch in ((48000, 16000, 2), (48000, 44100, 2), (44100, 16000, 1)):
+        S, n, m0, cnt = 3, 30011, 101, 7000
+        x = rng.standard_normal((S, n * ch + 6)).astype(np.float32)  # stride > one stream's samples
+        src = torch.from_numpy(x).cuda()
+        out_b = torch.zeros(S, cnt + 5, dtype=torch.float32, device="cuda")
+        gpu_engine.resample_batch(src.data_ptr(), x.shape[1], S, 17, n, ch, sr_in, sr_out, m0, cnt, out_b.data_ptr(),
+                                  cnt + 5)
+        for i in range(S):
+            one = torch.zeros(cnt, dtype=torch.float32, device="cuda")
+            gpu_engine.resample_range(src[i].data_ptr(), 17, n, ch, sr_in, sr_out, m0, cnt, one.data_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(out_b[i, :cnt], one), (sr_in, sr_out, ch, i)
+            assert not out_b[i, cnt:].any()
