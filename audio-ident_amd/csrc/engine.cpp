@@ -1374,7 +1374,8 @@ static int finalize_locked(aid_engine *e) {
     HIP_TRY(e->idx_off.reserve(K));
     HIP_TRY(e->scan_tmp.reserve(4 * (K / 1024 + 2) + 4096));
     HIP_TRY(e->idx_post.reserve((size_t)std::max<int64_t>(e->n_post, 1)));
-    HIP_TRY(e->idx_sig.reserve((size_t)std::max<int64_t>(e->n_post, 1)));
+    // + 8: K5's LDS path reads the signatures in aligned chunks of 4 or 8; a record's last chunk may reach past the end
+    HIP_TRY(e->idx_sig.reserve((size_t)std::max<int64_t>(e->n_post, 1) + 8));
     if (e->n_tracks == 0) HIP_TRY(e->tomb.reserve(1024));
     HIP_TRY(hipMemsetAsync(e->idx_cnt.p, 0, K * sizeof(uint32_t), s));
     HIP_TRY(e->nz.reserve(1));
@@ -1860,6 +1861,10 @@ constexpr double kForwardedPerBucket = 2.0;  // forwarded votes (1-bit filter es
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
 constexpr int kSpeculateQueries = 16;  // run_queries: LDS match path launched with the vote counts
+#ifndef AID_K5_MAXV_PER_CTR
+#define AID_K5_MAXV_PER_CTR 2  // A/B builds only (index.hip has the same bound)
+#endif
+constexpr int64_t kLdsMaxVotes = (int64_t)AID_K5_MAXV_PER_CTR << 16;  // index.hip k_match_lds: heavier -> global path
 
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
                        int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
@@ -1917,8 +1922,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         e->st_votes += h_votes[q];
         e->st_records += h_count[q];
     }
-    if (speculate)  // the LDS path ran every query once: two enumerations (counting, then the exact inserts)
-        for (int q = 0; q < nq; ++q) e->st_sig_reads += 2 * h_votes[q];
+    if (speculate)  // the LDS path ran every light query once: two enumerations (counting, then the exact inserts)
+        for (int q = 0; q < nq; ++q) e->st_sig_reads += h_votes[q] <= kLdsMaxVotes ? 2 * h_votes[q] : 0;
     // global histogram, sized for the votes that pass K5a's 2^20-bit seen filter (all but the
     // distinct bits: v - m(1 - e^{-v/m})) at ~2 per bucket: a chance bucket reaching
     // min_match - 1 then has probability ~1e-5. Sizing it for ALL votes (2 buckets each: 2 MB rows on
@@ -1938,10 +1943,12 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // On the v2 catalog (~84.5k votes per window, probes/k5_path_probe.py) it is the faster path (201k against
     // 185k clips/s, rows equal), so a batch goes to it when its mean query has <= 2^17 votes (2 per counter) and
     // none has more than 2^20 (a heavier one falls back to the global path after its LDS run)
-    double vsum = 0.0;
-    for (int q = 0; q < nq; ++q) vsum += (double)h_votes[q];
-    const bool lds_load = 2.0 * votes <= 65536.0 || (vsum / std::max(nq, 1) <= (double)(1 << 17) && votes <= (double)(1 << 20));
-    const bool fast = !speculate && (e->k5_path == 1 || (e->k5_path == 0 && lds_load));
+    // Each query is routed by its own vote count: k_match_lds answers the queries with <= kLdsMaxVotes
+    // (2 per 16-bit-indexed counter) and hands heavier ones straight back (nrows -1, no LDS run), so the batch takes
+    // the LDS launch whenever some query is light enough for it; the heavy ones run on the global path below
+    int n_light = 0;
+    for (int q = 0; q < nq; ++q) n_light += h_votes[q] <= kLdsMaxVotes;
+    const bool fast = !speculate && (e->k5_path == 1 || (e->k5_path == 0 && n_light > 0));
     // fast path: the whole vote filter in LDS (K5 `k_match_lds`); overflowed queries fall
     // through to the global-histogram path below
     if (fast) {
@@ -1964,10 +1971,11 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         }
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();
-        for (int q = 0; q < nq; ++q) e->st_sig_reads += 2 * h_votes[q];  // counting pass + insert pass (2 B each)
-        e->st_q_lds += nq;
+        for (int q = 0; q < nq; ++q)  // counting pass + insert pass (2 B each), light queries only
+            e->st_sig_reads += h_votes[q] <= kLdsMaxVotes ? 2 * h_votes[q] : 0;
+        e->st_q_lds += n_light;
     }
-    if (speculate) e->st_q_lds += nq;
+    if (speculate) e->st_q_lds += n_light;
     for (int attempt = 1; !todo.empty(); ++attempt, bits += 2) {
         for (int q : todo) e->st_post_reads += h_votes[q] * (parts + 1);  // K5a once per key partition, K5b once
         e->st_q_global += (int64_t)todo.size();

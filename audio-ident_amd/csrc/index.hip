@@ -575,21 +575,160 @@ constexpr int kFastTrackCap = AID_K5_TCAP;
 constexpr int kFastThreads = AID_K5_LDS_THREADS;
 
 static_assert(kLdsHistBits <= 16, "the LDS filter's buckets come from 16-bit posting signatures");
+// heaviest query the LDS path takes (2 votes per counter); heavier ones report nrows = -1 at once and the host runs
+// them on the global path (engine.cpp run_queries: kLdsMaxVotes there is the same bound)
+#ifndef AID_K5_MAXV_PER_CTR
+#define AID_K5_MAXV_PER_CTR 2  // A/B builds only (with engine.cpp's copy of the bound)
+#endif
+constexpr int64_t kLdsMaxVotes = (int64_t)AID_K5_MAXV_PER_CTR << kLdsHistBits;
 
-// every vote's LDS filter bucket, (sig - tq) mod 2^kLdsHistBits, for the calling wave's share of the records:
-// f(bucket) for live votes, U windows of signature loads in flight
-template <typename F>
-__device__ __forceinline__ void for_each_sig(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
-                                             F &&f) {
-    for_each_window<kLdsSigWindows>(qp, a, n, wave, nw, lane, [&](const uint32_t *pos, const int32_t *tqs, bool *ok) {
-        uint16_t sg[kLdsSigWindows];
+// The LDS path walks the records' postings in CHUNKS of kSigChunk (8 or 16 B of 2-B signatures, one load per lane):
+// a wave takes its share of the records (as for_each_window), scans their chunk counts -- a record at CSR positions
+// [p0, p1) covers the aligned chunks p0 / C .. (p1 + C - 1) / C -- and walks the concatenated chunks 64 at a time
+// (64 C postings per window) with U windows of loads in flight; a lane's C-bit mask says which of its chunk's
+// postings belong to the record (the first and last chunk of a record are partial). The per-window bookkeeping
+// (record cursor, positions) is paid once per 64 C votes instead of once per 64: with one posting per lane the walk
+// issued ~63 VALU + 32 SALU per 64 votes and was the LDS path's cost (r05e: without its second enumeration K5 took
+// 1.76 of 3.63 ms, without the first pass's LDS atomics 3.24).
+#ifndef AID_K5_CW
+#define AID_K5_CW 4  // A/B builds only: postings per chunk, 4 (8-B loads) or 8 (16-B loads)
+#endif
+constexpr int kSigChunk = AID_K5_CW;
+static_assert(kSigChunk == 4 || kSigChunk == 8, "signature chunks of 4 or 8 postings");
+typedef uint32_t sig_chunk_t __attribute__((ext_vector_type(kSigChunk / 2)));
+
+// one wave's group of <= 64 records: lane = record (CSR range [p0, p1), query time tq), chunk-count scan
+struct ChunkGroup {
+    uint32_t p0, p1, incl, excl, total;
+    int32_t tq;
+};
+
+__device__ __forceinline__ ChunkGroup load_group(const QueryParams &qp, int64_t a, int64_t n, int64_t base,
+                                                 int64_t chunk, int lane) {
+    ChunkGroup gr{0u, 0u, 0u, 0u, 0u, 0};
+    const int64_t i = base + lane;
+    uint32_t clen = 0;
+    if (lane < chunk && i < n) {
+        const uint64_t r = qp.recs[a + i];
+        const uint32_t k = key26((uint32_t)r);
+        gr.tq = (int32_t)(r >> 32);
+        gr.p0 = qp.offsets[k];
+        gr.p1 = qp.offsets[k + 1];
+        clen = gr.p1 > gr.p0 ? (gr.p1 + (kSigChunk - 1)) / kSigChunk - gr.p0 / kSigChunk : 0u;
+    }
+    uint32_t incl = clen;
 #pragma unroll
-        for (int u = 0; u < kLdsSigWindows; ++u) sg[u] = qp.sig[pos[u]];
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    gr.incl = incl;
+    gr.excl = incl - clen;
+    gr.total = __shfl(incl, 63);
+    return gr;
+}
+
+// g(cid[U], tq[U], vm[U]) for every window of the group: chunk index, query time and posting mask per lane
+template <int U, typename G>
+__device__ __forceinline__ void walk_group(const ChunkGroup &gr, int lane, G &&g) {
+    int r = 0;
+    uint32_t r_excl = __builtin_amdgcn_readlane(gr.excl, 0), r_incl = __builtin_amdgcn_readlane(gr.incl, 0);
+    uint32_t r_p0 = __builtin_amdgcn_readlane(gr.p0, 0), r_p1 = __builtin_amdgcn_readlane(gr.p1, 0);
+    int32_t r_tq = __builtin_amdgcn_readlane(gr.tq, 0);
+    auto next_rec = [&]() {
+        ++r;
+        r_excl = __builtin_amdgcn_readlane(gr.excl, r);
+        r_incl = __builtin_amdgcn_readlane(gr.incl, r);
+        r_p0 = __builtin_amdgcn_readlane(gr.p0, r);
+        r_p1 = __builtin_amdgcn_readlane(gr.p1, r);
+        r_tq = __builtin_amdgcn_readlane(gr.tq, r);
+    };
+    // chunk c of the record [rp0, rp1): mask of its postings C c + e inside the record
+    constexpr uint32_t kAll = (1u << kSigChunk) - 1;
+    auto maskc = [](uint32_t c, uint32_t rp0, uint32_t rp1) -> uint32_t {
+        const int s0 = (int)rp0 - (int)(kSigChunk * c), s1 = (int)rp1 - (int)(kSigChunk * c);
+        const int lo = min(max(s0, 0), kSigChunk), hi = min(max(s1, 0), kSigChunk);
+        return (kAll << lo) & ~(kAll << hi) & kAll;
+    };
+    const uint32_t total = gr.total;
+    for (uint32_t w0 = 0; w0 < total; w0 += 64u * U) {
+        uint32_t cid[U], vm[U];
+        int32_t tqs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t lo = w0 + 64u * u, j = lo + lane;
+            cid[u] = 0;
+            vm[u] = 0;
+            tqs[u] = 0;
+            if (lo >= total) continue;  // uniform
+            while (r_incl <= lo) next_rec();  // r < 63 here: incl of lane 63 is total > lo
+            if (r_incl >= lo + 64u) {  // the whole window inside record r (uniform)
+                cid[u] = r_p0 / kSigChunk + (j - r_excl);
+                tqs[u] = r_tq;
+                vm[u] = maskc(cid[u], r_p0, r_p1);
+            } else {
+                for (;;) {  // records r, r+1, ... up to the one holding chunk lo + 63 (or the last)
+                    if (j >= r_excl && j < r_incl) {
+                        cid[u] = r_p0 / kSigChunk + (j - r_excl);
+                        tqs[u] = r_tq;
+                        vm[u] = maskc(cid[u], r_p0, r_p1);
+                    }
+                    if (r_incl >= lo + 64u || r == 63) break;
+                    next_rec();
+                }
+            }
+        }
+        g(cid, tqs, vm);
+    }
+}
+
+// records per wave group: ceil(n / (waves x rounds)) <= 64, rounds = ceil(n / (64 waves)) (as for_each_window)
+__device__ __forceinline__ int64_t group_records(int64_t n, int nw) {
+    const int64_t rounds = (n + (int64_t)nw * 64 - 1) / ((int64_t)nw * 64);
+    return rounds ? (n + nw * rounds - 1) / (nw * rounds) : 64;
+}
+
+template <int U, typename G>
+__device__ __forceinline__ void for_each_chunk(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
+                                               G &&g) {
+    const int64_t chunk = group_records(n, nw);
+    for (int64_t base = (int64_t)wave * chunk; base < n; base += (int64_t)nw * chunk)
+        walk_group<U>(load_group(qp, a, n, base, chunk, lane), lane, g);
+}
+
+// the signatures of one window's chunks, element e of the lane's chunk: (sig_e - tq) mod 2^bits = the LDS bucket
+__device__ __forceinline__ sig_chunk_t load_sigs(const QueryParams &qp, uint32_t cid) {
+    return reinterpret_cast<const sig_chunk_t *>(qp.sig)[cid];
+}
+__device__ __forceinline__ uint32_t sig_bucket(const sig_chunk_t &v, int e, int32_t tq) {
+    return ((uint32_t)(v[e >> 1] >> (16 * (e & 1))) - (uint32_t)tq) & ((1u << kLdsHistBits) - 1);
+}
+
+// every live vote's LDS filter bucket for the calling wave's records: f(bucket), U windows in flight; with `one`
+// (the wave's records are ONE group, `grp`, loaded once for both passes) the group's record loads are not repeated
+template <typename F>
+__device__ __forceinline__ void sig_votes(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
+                                          bool one, const ChunkGroup &grp, F &&f) {
+    auto g = [&](const uint32_t *cid, const int32_t *tqs, const uint32_t *vm) {
+        sig_chunk_t sw[kLdsSigWindows];
+#pragma unroll
+        for (int u = 0; u < kLdsSigWindows; ++u) sw[u] = load_sigs(qp, cid[u]);
 #pragma unroll
         for (int u = 0; u < kLdsSigWindows; ++u)
-            if (ok[u]) f((uint32_t)(sg[u] - (uint32_t)tqs[u]) & ((1u << kLdsHistBits) - 1));
-    });
+#pragma unroll
+            for (int e = 0; e < kSigChunk; ++e)
+                if ((vm[u] >> e) & 1u) f(sig_bucket(sw[u], e, tqs[u]));
+    };
+    if (one) walk_group<kLdsSigWindows>(grp, lane, g);
+    else for_each_chunk<kLdsSigWindows>(qp, a, n, wave, nw, lane, g);
 }
+
+#ifndef AID_K5_HOTQ
+#define AID_K5_HOTQ 1  // A/B builds only: 0 = each hot vote's posting loaded inside the walk
+#endif
+// hot votes queued by the insert pass (posting index, tq): the LDS the counters leave beside the exact table
+constexpr int kTableBytes = kFastVoteCap * (8 + 3 * 4) + kFastTrackCap * (4 + 8);
+constexpr int kHotQueue = ((1 << kLdsHistBits) / kLdsCtrPerWord * 4 - kTableBytes) / 8;
 
 struct FastLds {
     union {
@@ -599,11 +738,14 @@ struct FastLds {
             uint32_t vcnt[kFastVoteCap], vmin[kFastVoteCap], vmax[kFastVoteCap];
             uint32_t tkey[kFastTrackCap];
             unsigned long long tbest[kFastTrackCap];
+            uint2 hq[kHotQueue > 0 ? kHotQueue : 1];  // the insert pass's hot votes (posting index, tq)
         } t;
     } u;
     uint32_t hot[(1 << kLdsHistBits) / 32];
-    int32_t out_n, overflow;
+    int32_t out_n, overflow, hq_n;
 };
+static_assert(kHotQueue >= 256 && sizeof(FastLds::u) == (1 << kLdsHistBits) / kLdsCtrPerWord * 4,
+              "the hot-vote queue lives in the counters' LDS beside the exact table");
 
 __global__ __launch_bounds__(kFastThreads)
 #if AID_K5_LDS8
@@ -615,28 +757,45 @@ __attribute__((amdgpu_waves_per_eu(AID_K5_WPE)))
 void k_match_lds(QueryParams qp) {
     __shared__ FastLds L;  // 8-bit counters: 72 KB, two workgroups per CU (16-bit: 136 KB, one)
     const int q = blockIdx.x;
+    // a query heavier than the LDS filter suits goes to the global path at once, by its own vote count (a heavy
+    // query here would wrap many 8-bit counters, mark their buckets hot and likely overflow the exact table after a
+    // slow run); uniform, before any barrier
+    if (qp.votes[q] > kLdsMaxVotes) {
+        if (threadIdx.x == 0) qp.nrows[q] = -1;
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = kFastThreads / 64;
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t mm = (uint32_t)qp.min_match;
-    const uint32_t hmask = (1u << kLdsHistBits) - 1;
     for (int i = tid; i < (1 << kLdsHistBits) / kLdsCtrPerWord; i += kFastThreads) L.u.hist[i] = 0u;
     if (AID_K5_LDS8)
         for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
-    if (tid == 0) { L.out_n = 0; L.overflow = 0; }
+    if (tid == 0) { L.out_n = 0; L.overflow = 0; L.hq_n = 0; }
     __syncthreads();
     // the query's exact vote total (k_query_votes): below the counter maximum no counter can wrap, so only
     // heavier queries pay for returning atomics (the carry check below)
     const bool check_wrap = qp.votes[q] >= (int64_t)kLdsCtrMax;
+    // a query whose records fit one group per wave (<= 64 x waves: config 4's ~650) loads them once for both passes
+#ifndef AID_K5_REUSE
+#define AID_K5_REUSE 1  // A/B builds only
+#endif
+    ChunkGroup grp_one{0u, 0u, 0u, 0u, 0u, 0};
+    const bool one_group = AID_K5_REUSE && n <= (int64_t)nw * 64;
+    if (one_group) {
+        const int64_t chunk = group_records(n, nw);
+        grp_one = load_group(qp, a, n, (int64_t)wave * chunk, chunk, lane);
+    }
+
 #ifndef AID_K5_DIAG
 #define AID_K5_DIAG 0  // timing-only builds (wrong rows): 1 = phase 1 without its LDS atomics, 2 = no phase 3, 3 = both
 #endif
 #if AID_K5_DIAG & 1
     uint32_t diag_x = 0;
-    for_each_sig(qp, a, n, wave, nw, lane, [&](uint32_t h) { diag_x += h; });
+    sig_votes(qp, a, n, wave, nw, lane, one_group, grp_one, [&](uint32_t h) { diag_x += h; });
     if (diag_x == 0xFFFFFFFFu) L.overflow = 2;  // keeps the loads
 #else
     // phase 1: every vote counted from its posting's 2-B signature alone (bucket = sig - tq = H(track) + d)
-    for_each_sig(qp, a, n, wave, nw, lane, [&](uint32_t h) {
+    sig_votes(qp, a, n, wave, nw, lane, one_group, grp_one, [&](uint32_t h) {
         const uint32_t sh = kLdsCtrBits * (h % kLdsCtrPerWord);
         uint32_t *w = &L.u.hist[h / kLdsCtrPerWord];
         if (check_wrap) {
@@ -709,30 +868,53 @@ void k_match_lds(QueryParams qp) {
         }
     };
     // phase 3: the signatures again; only a vote whose bucket is hot reads its 8-B posting and enters the table
-    if (!(AID_K5_DIAG & 2))
-    for_each_window<kLdsSigWindows>(qp, a, n, wave, nw, lane, [&](const uint32_t *pos, const int32_t *tqs, bool *ok) {
-        uint16_t sg[kLdsSigWindows];
+    auto insert_pass = [&](const uint32_t *cid, const int32_t *tqs, const uint32_t *vm) {
+        sig_chunk_t sw[kLdsSigWindows];
 #pragma unroll
-        for (int u = 0; u < kLdsSigWindows; ++u) sg[u] = qp.sig[pos[u]];
-        bool hot[kLdsSigWindows];
-        uint64_t e[kLdsSigWindows];
+        for (int u = 0; u < kLdsSigWindows; ++u) sw[u] = load_sigs(qp, cid[u]);
+        uint32_t hm[kLdsSigWindows];  // the chunk's postings whose bucket is hot
 #pragma unroll
         for (int u = 0; u < kLdsSigWindows; ++u) {
-            const uint32_t h = (uint32_t)(sg[u] - (uint32_t)tqs[u]) & hmask;
-            hot[u] = ok[u] && ((L.hot[h >> 5] >> (h & 31)) & 1u);
-            e[u] = 0;
+            hm[u] = 0;
+#pragma unroll
+            for (int e = 0; e < kSigChunk; ++e) {
+                const uint32_t h = sig_bucket(sw[u], e, tqs[u]);
+                hm[u] |= ((vm[u] >> e) & (L.hot[h >> 5] >> (h & 31)) & 1u) << e;
+            }
         }
 #pragma unroll
-        for (int u = 0; u < kLdsSigWindows; ++u)  // the rare hot votes' postings, all issued before any is used
-            if (hot[u]) e[u] = qp.post[pos[u]];
-#pragma unroll
-        for (int u = 0; u < kLdsSigWindows; ++u) {
-            if (!hot[u]) continue;
-            const uint32_t tr = (uint32_t)e[u];
+        for (int u = 0; u < kLdsSigWindows; ++u)
+            while (hm[u]) {  // rare: each hot vote is queued in LDS; its posting is read after the walk
+                const int e = __builtin_ctz(hm[u]);
+                hm[u] &= hm[u] - 1;
+                const uint32_t pi = (uint32_t)kSigChunk * cid[u] + (uint32_t)e;
+                const int slot = AID_K5_HOTQ ? atomicAdd(&L.hq_n, 1) : kHotQueue;
+                if (slot < kHotQueue) {
+                    L.u.t.hq[slot] = make_uint2(pi, (uint32_t)tqs[u]);
+                } else {  // queue full: this vote's posting now (a dependent load: one memory latency)
+                    const uint64_t pv = qp.post[pi];
+                    const uint32_t tr = (uint32_t)pv;
+                    if (!(qp.tomb_live && qp.tomb[tr])) insert(tr, (int32_t)(pv >> 32) - tqs[u], tqs[u]);
+                }
+            }
+    };
+    if (!(AID_K5_DIAG & 2)) {
+        if (one_group) walk_group<kLdsSigWindows>(grp_one, lane, insert_pass);
+        else for_each_chunk<kLdsSigWindows>(qp, a, n, wave, nw, lane, insert_pass);
+    }
+    __syncthreads();
+    // the queued hot votes: every thread loads its entries' postings at once (one memory latency for the whole
+    // queue instead of one per hot vote inside the walk), then inserts them
+    {
+        const int nh = min(L.hq_n, kHotQueue);
+        for (int i = tid; i < nh; i += kFastThreads) {
+            const uint2 h = L.u.t.hq[i];
+            const uint64_t pv = qp.post[h.x];
+            const uint32_t tr = (uint32_t)pv;
             if (qp.tomb_live && qp.tomb[tr]) continue;  // a removed track's vote (the filter counted it: superset)
-            insert(tr, (int32_t)(e[u] >> 32) - tqs[u], tqs[u]);
+            insert(tr, (int32_t)(pv >> 32) - (int32_t)h.y, (int32_t)h.y);
         }
-    });
+    }
     __syncthreads();
     // phase 4: best d per track
     for (int s = tid; s < kFastVoteCap; s += kFastThreads) {

@@ -20,10 +20,20 @@ Extra keys of the line (none of them is `value`):
     extraction kernel, from the newest committed profiles/;
   * fullband -- the same batch with partials up to 20 kHz (no cold upper blocks);
   * catalog -- BASELINE config 3: 100k x 30 s tracks sharded over the ranks, extract +
-    the RCCL all-gather of the postings (aid_index_allgather) + the index build; its exact_lane
-    sub-key is BASELINE config 4 against that index (8192 noisy 5 s clips per rank, aid_exact_lane);
+    the RCCL all-gather of the postings (aid_index_allgather) + the index build, then the replicas
+    checked (replicas_identical: device checksums compared across ranks; shard_parity: 8 tracks of
+    every rank's shard against the oracle on rank 0); its exact_lane sub-key is BASELINE config 4
+    against that index (10k + 1k noisy 5 s clips per rank, aid_exact_lane), with parity: 64 of the
+    timed clips checked against the oracle at the catalog's scale (records, K5 rows on every path,
+    the lane's rows against an all-oracle lane);
+  * service -- the drop-in olaf_query path through the query coalescer at 1 / 16 / 64 clients;
+  * stream -- BASELINE config 5 at serving scale: 256 live 48 kHz stereo streams per rank through
+    aidfp.stream.StreamBank (one batched K6 + one windowed K1-K5 call per 2.5 s push), with parity
+    of the first windows against the oracle route;
   * cpu_baseline -- the bit-exact C oracle on the host cores, and the NumPy/SciPy path, on
     rank 0 at N=1 over bounded samples of the same clips.
+A failed check (headline parity, catalog checks, stream parity) exits 1; a leg that hangs past
+--leg-deadline exits 3 after the line is printed.
 """
 
 from __future__ import annotations

@@ -51,3 +51,35 @@ def test_rows_equal_oracle_under_load(per_hash, path):
             ref = O.query(post, r, min_match=eng.min_match, max_rows=eng.max_results)
             assert np.array_equal(g, ref), (per_hash, g[:4], ref[:4])
             assert len(g) and g[0, 1] == 7
+
+
+def test_mixed_batch_routes_each_query_by_its_votes():
+    """in one batch, queries above the LDS filter's bound (2^17 votes) go straight to the global path
+    while the light ones are answered in LDS; rows equal the oracle's either way."""
+    rng = np.random.default_rng(11)
+    track = synth.synth(7, 0, 30 * SR, SR)
+    trec = O.fingerprint(track, HOP)
+    q = synth.synth(7, SR * 9, 5 * SR, SR, snr_db=20.0, salt=5)
+    qrec = O.fingerprint(q, HOP)
+    qh = np.unique((qrec & np.uint64(0xFFFFFFFF)).astype(np.uint32))
+    per_hash = 300
+    H = np.ascontiguousarray(np.concatenate([(trec & np.uint64(0xFFFFFFFF)).astype(np.uint32), np.repeat(qh, per_hash)]))
+    TR = np.ascontiguousarray(np.concatenate([np.full(len(trec), 7, np.uint32),
+                                              rng.integers(1000, 9000, len(qh) * per_hash).astype(np.uint32)]))
+    T = np.ascontiguousarray(np.concatenate([(trec >> np.uint64(32)).astype(np.uint32),
+                                             rng.integers(0, 3000, len(qh) * per_hash).astype(np.uint32)]))
+    heavy = [qrec, qrec[::-1].copy()]
+    light = [qrec[:60], qrec[200:260]]
+    with Engine(SR) as eng:
+        eng.index_add_postings(H.ctypes.data, TR.ctypes.data, T.ctypes.data, len(H), device=False)
+        eng.index_finalize()
+        post = eng.index_export()
+        qs = [heavy[0], light[0], heavy[1], light[1]] + [qrec[i:i + 40] for i in range(0, 600, 40)]
+        eng.match_stats(reset=True)
+        got = eng.query(qs)
+        st = eng.match_stats(reset=True)
+        for g, r in zip(got, qs):
+            assert np.array_equal(g, O.query(post, r, min_match=eng.min_match, max_rows=eng.max_results))
+        votes_heavy = len(qrec) * per_hash
+        assert votes_heavy > (1 << 17)
+        assert st["queries_global"] == 2 and st["queries_lds"] == len(qs) - 2, st
