@@ -15,7 +15,10 @@ constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 
 // K1: kStftWaves waves per workgroup, one workgroup per CU: 16 waves (4 per SIMD at <= 128 VGPRs),
 // each with a private exchange buffer, + 24.5 KB of tables fit the 160 KB LDS
-constexpr int kStftWaves = 16;
+#ifndef AID_K1_WAVES
+#define AID_K1_WAVES 16  // A/B builds only (engine.cpp and stft.hip alike)
+#endif
+constexpr int kStftWaves = AID_K1_WAVES;
 constexpr int kStftStrip = 16;   // frames per wave at least, for large batches (one ring fill per range)
 constexpr int kK1MinFrames = 2;  // frames per wave at least, for small batches
 // float2 entries of a wave's exchange buffer: E1's 32 regions of 64 dwords at shifted bases (2108 dwords),
@@ -74,6 +77,12 @@ __host__ __device__ constexpr uint32_t bucket_key(uint32_t h) {
 __host__ __device__ constexpr uint16_t posting_sig(uint32_t track, uint32_t t) {
     return (uint16_t)(((track * 0x9E3779B1u) >> 16) + t);
 }
+
+// K5: the heaviest query (exact votes, k_query_votes) the LDS match path takes; heavier ones go straight to the
+// global-histogram path (engine.cpp run_queries routes them, k_match_lds hands any back at once). 8 votes per
+// counter of its 2^15-bucket filter: on config 4 (~84.5 k votes per window, a few up to ~2^18) every query stays in
+// LDS, where the 132 of 36,864 heaviest ones had cost 0.3 ms per 4096-clip call on the global path at 2^17.
+constexpr int64_t kLdsMaxVotes = (int64_t)1 << 18;
 
 // K3: anchor frames per chunk; peaks in (chunk + zone) frames fit LDS
 constexpr int kHashChunk = 1024;

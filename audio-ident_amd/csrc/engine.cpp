@@ -1861,10 +1861,6 @@ constexpr double kForwardedPerBucket = 2.0;  // forwarded votes (1-bit filter es
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
 constexpr int kSpeculateQueries = 16;  // run_queries: LDS match path launched with the vote counts
-#ifndef AID_K5_MAXV_PER_CTR
-#define AID_K5_MAXV_PER_CTR 2  // A/B builds only (index.hip has the same bound)
-#endif
-constexpr int64_t kLdsMaxVotes = (int64_t)AID_K5_MAXV_PER_CTR << 16;  // index.hip k_match_lds: heavier -> global path
 
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
                        int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {

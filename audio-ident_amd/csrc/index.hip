@@ -531,56 +531,52 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     if (tid == 0) qp.nrows[q] = (overflow || out_n > kTrackCap) ? -1 : min(n, qp.max_rows);
 }
 
-// ---- K5 (fast path): the whole vote filter in LDS, one 1024-thread workgroup per query ----
-// Phase 1: 2^16 16-bit hashed counters of (track, d) votes (128 KB of LDS); each wave
-//          takes one query record at a time and its 64 lanes stride over that record's
-//          posting list (coalesced 512-byte reads).
-// Phase 2: counters >= min_match -> a 2^16-bit "hot" bitmap (8 KB).
-// Phase 3: the counter region is reused as the exact (track, d) table; only votes whose
-//          bucket is hot are inserted (exact superset filter, as in K5a/K5b).
-// Phase 4: best d per track, rank, write rows (same as K5b). Any table overflow, or a
-//          16-bit counter reaching 0xFFFF, reports nrows = -1 and the host re-runs the query
-//          on the global-histogram path.
-// 8-bit counters (64 KB) and a 2048-entry exact table: two workgroups per CU, so one query's
-// barriers and table phases overlap another's posting reads. (Four 512-thread workgroups with 2^15 counters and a
-// 1024-entry table ran K5 2.5 % faster on config 4 but sent a bench query to the global path: dropped.) A counter that wraps past 255 marks
-// its bucket hot at once (>= 256 votes), as does any full counter its carry runs through, so the
-// filter stays an exact superset; with 16-bit counters (one workgroup per CU) a wrap hands the
-// query to the global path.
+// ---- K5 (fast path): the whole vote filter in LDS, one 512-thread workgroup per query, four per CU ----
+// Phase 1: every vote counted in 2^15 8-bit hashed counters (32 KB of LDS) from its posting's 2-B signature alone
+//          (bucket = sig - tq = H(track) + d: aidfp_layout.h posting_sig); the waves walk their records' signatures
+//          in 8-posting chunks (one 16-B load per lane, for_each_chunk).
+// Phase 2: counters >= min_match -> a 2^15-bit "hot" bitmap (4 KB).
+// Phase 3: the counter region is reused as the exact (track, d) table; the signatures are walked again and only a
+//          vote whose bucket is hot is queued (posting index, tq) in the LDS the table leaves free; after the walk
+//          every thread reads its queued votes' 8-B postings at once and inserts them (exact superset filter, as in
+//          K5a/K5b).
+// Phase 4: best d per track, rank, write rows (same as K5b). Any table overflow reports nrows = -1 and the host
+//          re-runs the query on the global-histogram path; a query above kLdsMaxVotes is handed back at once.
+// A counter that wraps past 255 marks its bucket hot at once (>= 256 votes), as does any full counter its carry
+// runs through, so the filter stays an exact superset. Round 5 (config 4, per 4096-clip lane call, same-box A/Bs
+// r05d-r05i): 8-B postings walked one per lane, 2^16 counters, two 1024-thread workgroups per CU 3.60-3.73 ms ->
+// 2-B signatures one per lane 3.64-3.74 (bytes were not the bound: the walk's ~95 instructions per 64 votes were)
+// -> 4-posting chunks 2.71-2.76 -> hot-vote queue 2.68 -> 8-posting chunks, four 512-thread workgroups per CU, the
+// LDS path up to 2^18 votes per query 1.80-1.86.
 #ifndef AID_K5_LDS8
 #define AID_K5_LDS8 1  // A/B builds only: 0 = 16-bit counters
 #endif
 #ifndef AID_K5_LDS_THREADS
-#define AID_K5_LDS_THREADS 1024
+#define AID_K5_LDS_THREADS 512
 #endif
 #ifndef AID_K5_SIG_U
-#define AID_K5_SIG_U 4  // A/B builds only (6 and 8 spill at the 64 VGPRs of 8 waves per SIMD)
+#define AID_K5_SIG_U 3  // A/B builds only (more spill at the 64 VGPRs of 8 waves per SIMD)
 #endif
 constexpr int kLdsSigWindows = AID_K5_SIG_U;  // windows of 64 two-byte signature loads a wave keeps in flight
 #ifndef AID_K5_HBITS
-#define AID_K5_HBITS 16  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
+#define AID_K5_HBITS 15  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
 #endif
 constexpr int kLdsHistBits = AID_K5_HBITS;
 constexpr int kLdsCtrBits = AID_K5_LDS8 ? 8 : 16;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
 #ifndef AID_K5_VCAP
-#define AID_K5_VCAP (AID_K5_LDS8 ? 2048 : 4096)
+#define AID_K5_VCAP (AID_K5_LDS8 ? 1024 : 4096)
 #endif
 constexpr int kFastVoteCap = AID_K5_VCAP;
 #ifndef AID_K5_TCAP
-#define AID_K5_TCAP 1024
+#define AID_K5_TCAP 512
 #endif
 constexpr int kFastTrackCap = AID_K5_TCAP;
 constexpr int kFastThreads = AID_K5_LDS_THREADS;
 
 static_assert(kLdsHistBits <= 16, "the LDS filter's buckets come from 16-bit posting signatures");
-// heaviest query the LDS path takes (2 votes per counter); heavier ones report nrows = -1 at once and the host runs
-// them on the global path (engine.cpp run_queries: kLdsMaxVotes there is the same bound)
-#ifndef AID_K5_MAXV_PER_CTR
-#define AID_K5_MAXV_PER_CTR 2  // A/B builds only (with engine.cpp's copy of the bound)
-#endif
-constexpr int64_t kLdsMaxVotes = (int64_t)AID_K5_MAXV_PER_CTR << kLdsHistBits;
+// kLdsMaxVotes (aidfp_layout.h): a heavier query reports nrows = -1 at once and the host runs it on the global path
 
 // The LDS path walks the records' postings in CHUNKS of kSigChunk (8 or 16 B of 2-B signatures, one load per lane):
 // a wave takes its share of the records (as for_each_window), scans their chunk counts -- a record at CSR positions
@@ -591,7 +587,7 @@ constexpr int64_t kLdsMaxVotes = (int64_t)AID_K5_MAXV_PER_CTR << kLdsHistBits;
 // issued ~63 VALU + 32 SALU per 64 votes and was the LDS path's cost (r05e: without its second enumeration K5 took
 // 1.76 of 3.63 ms, without the first pass's LDS atomics 3.24).
 #ifndef AID_K5_CW
-#define AID_K5_CW 4  // A/B builds only: postings per chunk, 4 (8-B loads) or 8 (16-B loads)
+#define AID_K5_CW 8  // A/B builds only: postings per chunk, 4 (8-B loads) or 8 (16-B loads)
 #endif
 constexpr int kSigChunk = AID_K5_CW;
 static_assert(kSigChunk == 4 || kSigChunk == 8, "signature chunks of 4 or 8 postings");
@@ -750,7 +746,7 @@ static_assert(kHotQueue >= 256 && sizeof(FastLds::u) == (1 << kLdsHistBits) / kL
 __global__ __launch_bounds__(kFastThreads)
 #if AID_K5_LDS8
 #ifndef AID_K5_WPE
-#define AID_K5_WPE (2 * AID_K5_LDS_THREADS / 256)
+#define AID_K5_WPE 8
 #endif
 __attribute__((amdgpu_waves_per_eu(AID_K5_WPE)))
 #endif

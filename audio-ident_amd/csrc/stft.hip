@@ -113,7 +113,7 @@ __device__ __forceinline__ float2 pcm_ld(const aid_f2u &r) {
 __device__ __forceinline__ int e3q_slot(int k) { return 4 * (k & 255) + ((k >> 8) ^ (2 * ((k >> 3) & 1))); }
 
 template <bool LOGMAG, int ROWS>
-__global__ __launch_bounds__(kStftWaves * 64) void k_stft_power(const float *__restrict__ pcm,
+__global__ __launch_bounds__(kStftWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_stft_power(const float *__restrict__ pcm,
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
                                                                 int64_t total, int64_t n_waves,
                                                                 const Tables *__restrict__ tab, float *__restrict__ out,

@@ -40,6 +40,7 @@ from __future__ import annotations
 
 import argparse
 import datetime
+import gc
 import json
 import os
 import socket
@@ -796,7 +797,15 @@ def stream_leg(args, rank, world, dist, torch) -> dict:
 
         def local():
             run(S, False)  # warm-up: first-use allocations of the bank and the engine's scratch
-            return run(S, True)
+            # a serving process moves its start-up objects out of the cyclic collector's reach (gc.freeze), as a
+            # long-running server does after start-up: a full collection over this process's ~10^6 objects (torch, the
+            # legs before) otherwise lands inside some push (a 70 ms push in r05j, all of it outside the engine calls)
+            gc.collect()
+            gc.freeze()
+            try:
+                return run(S, True)
+            finally:
+                gc.unfreeze()
 
         wall, lat, res, tim, mst = _agreed(local, "stream (pushes)", dist)
         worst = int(np.argmax(lat))
@@ -937,6 +946,8 @@ def service_leg(args, rank, world, dist, torch) -> dict:
                 res = {}
                 for _ in range(8):  # warm: first-use allocations of the largest batch shape
                     svc.query(reqs[0])
+                gc.collect()  # start-up objects out of the cyclic collector's reach, as a serving process does
+                gc.freeze()
                 for c in levels:
                     lat = np.zeros(n_req)
                     hits = np.zeros(n_req, dtype=bool)
@@ -963,6 +974,7 @@ def service_leg(args, rank, world, dist, torch) -> dict:
                                    **{f"p{q}_ms": round(1e3 * float(np.percentile(lat, q)), 3) for q in (50, 95, 99)},
                                    "mean_batch": round(float(b.mean()), 2) if len(b) else 0.0,
                                    "top1": round(float(hits.mean()), 4)}
+                gc.unfreeze()
                 return res
 
             res = _agreed(run_levels, "service (queries)", dist)

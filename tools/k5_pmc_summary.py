@@ -8,11 +8,12 @@ bench.py reads (load_pmc_k5):
     -> profiles/pmc_TAG_k5.json, profiles/TAG_k5_kernel_stats.csv
 
 Only the full exact-lane calls are summarised: the dispatches whose grid is the largest one seen for k_match_lds
-(4096 clips x 3 sub-windows = 12288 workgroups of 1024 threads). Per call: each K5 kernel's mean duration (trace)
+(4096 clips x 3 sub-windows = 12288 workgroups, one per query). Per call: each K5 kernel's mean duration (trace)
 and its FETCH_SIZE / WRITE_SIZE bytes (raw counter values x 1 KiB; FETCH_SIZE counts the L2's fabric-side read
 requests, Infinity-Cache hits included, so it bounds the HBM reads from above). `fetch_factor` converts FETCH_SIZE to
 bytes for the kernel's access width: 2 for 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM), and the value
-the probes/fetch_calib.hip calibration measured for 8-B-per-lane reads when RUNDIR/calib.json exists.
+the probes/fetch_calib.hip calibration measured (RUNDIR/calib.json, else profiles/fetch_calib_r05b.json: 2 for 4-,
+8- and 16-B-per-lane reads).
 """
 import csv
 import json
@@ -32,11 +33,11 @@ def short(name: str) -> str:
 def main() -> None:
     tag, run = sys.argv[1], Path(sys.argv[2])
     trace = list(csv.DictReader(open(run / "trace" / "run_kernel_trace.csv", newline="")))
-    lds_grids = [int(r["Grid_Size_X"]) for r in trace if short(r["Kernel_Name"]) == "k_match_lds"]
-    if not lds_grids:
+    lds = [(int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"])) for r in trace if short(r["Kernel_Name"]) == "k_match_lds"]
+    if not lds:
         raise SystemExit("no k_match_lds dispatch in the trace")
-    g_lds = max(lds_grids)
-    queries = g_lds // 1024
+    g_lds, wg = max(lds)
+    queries = g_lds // wg  # one workgroup per query
     # the other kernels of a full lane call, by their grid for that many queries
     full_grid = {"k_match_lds": g_lds, "k_query_votes": queries * 256, "k_exact_consensus": None}
     dur = defaultdict(list)
@@ -58,8 +59,10 @@ def main() -> None:
             if k in full_grid and int(r["Grid_Size"]) == full_grid[k] and r["Counter_Name"] == cname:
                 ctr[(k, cname)].append(float(r["Counter_Value"]) * 1024.0)
     calib = None
-    if (run / "calib.json").exists():
-        calib = json.loads((run / "calib.json").read_text())
+    for c in (run / "calib.json", ROOT / "profiles" / "fetch_calib_r05b.json"):
+        if c.exists():
+            calib = json.loads(c.read_text())
+            break
     f8 = float(calib["fetch_factor_8B"]) if calib else None
     kernels = {}
     for k in full_grid:
