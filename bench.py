@@ -138,7 +138,7 @@ def load_sq() -> tuple[dict, str | None]:
                     out.setdefault(parts[1], {})[parts[2]] = float(parts[-1][5:])
         except Exception:
             continue
-        if any("SQ_INSTS_VALU" in v for v in out.values()):
+        if "SQ_INSTS_VALU" in out.get(KERNEL_SQ["stft_power"], {}):  # an extraction-kernel summary
             return out, f.name
     return {}, None
 
