@@ -5,6 +5,8 @@ beside it; a 12-wave K1 (AID_K1_WAVES=12 build: 125,824 B, 3 waves per SIMD at 1
 workgroup (21 KB, 124 VGPRs) per CU. The probe runs the bench's 256 x 10 s batch as
   single: one engine, one stream, 256 clips per step (the bench's step);
   dual:   two engines on two streams, 128 clips each, issued alternately, so engine B's K1 can overlap engine A's K2/K3;
+  alt:    whole 256-clip steps alternating between two engines on two streams (one step's kernel tails overlap the
+          next step's first kernels);
 and reports ms per step (256 clips) for each, after the bench's clock settle. The records of both modes must be equal.
 
     python probes/dual_stream_probe.py [--steps 40]
@@ -53,19 +55,28 @@ def main():
             b.extract_device(pcm.data_ptr(), offs_b, sb.cuda_stream)
         torch.cuda.synchronize()
 
+    def alt(k):  # whole steps alternating between two engines on two streams: kernel tails of one step overlap
+        for i in range(k):  # the next step's first kernels
+            if i % 2 == 0:
+                a.extract_device(pcm.data_ptr(), offs, sa.cuda_stream)
+            else:
+                b.extract_device(pcm.data_ptr(), offs, sb.cuda_stream)
+        torch.cuda.synchronize()
+
     def timed(fn, k):
         t = time.perf_counter()
         fn(k)
         return (time.perf_counter() - t) / k * 1e3
 
     out = {"k1_waves_per_cu": None, "rounds": []}
-    for fn in (single, dual):  # warm-up + clock settle
-        fn(3)
+    for fn in (single, dual, alt):  # warm-up + clock settle
+        fn(4)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.2:
         single(10)
     for _ in range(3):
-        out["rounds"].append({"single_ms": round(timed(single, args.steps), 4), "dual_ms": round(timed(dual, args.steps), 4)})
+        out["rounds"].append({"single_ms": round(timed(single, args.steps), 4), "dual_ms": round(timed(dual, args.steps), 4),
+                              "alt_ms": round(timed(alt, args.steps), 4)})
     single(1)
     ref = [a.hashes(c) for c in range(CLIPS)]
     dual(1)
@@ -73,6 +84,10 @@ def main():
     out["records_equal"] = all(np.array_equal(x, y) for x, y in zip(ref, got))
     out["single_ms"] = min(r["single_ms"] for r in out["rounds"])
     out["dual_ms"] = min(r["dual_ms"] for r in out["rounds"])
+    out["alt_ms"] = min(r["alt_ms"] for r in out["rounds"])
+    alt(2)
+    got_alt = [b.hashes(c) for c in range(CLIPS)]
+    out["records_equal_alt"] = all(np.array_equal(x, y) for x, y in zip(ref, got_alt))
     out["audio_s_per_s_single"] = round(CLIPS * CLIP_S / out["single_ms"] * 1e3, 1)
     out["audio_s_per_s_dual"] = round(CLIPS * CLIP_S / out["dual_ms"] * 1e3, 1)
     a.close()
