@@ -11,7 +11,8 @@ Here the index lives in one GPU engine:
     waiting request, collects whatever else arrives within `window_s` (up to `max_batch`),
     runs the batch under the read lock and resolves every request's future. Under load the
     next batch accumulates while the current one runs on the GPU, so batching follows the
-    arrival rate and a lone request pays at most `window_s` extra.
+    arrival rate. The window only opens after a batch of more than one request: at low load
+    (the previous batch was a lone request) a request is dispatched at once and pays no window.
 """
 
 from __future__ import annotations
@@ -105,6 +106,7 @@ class QueryCoalescer:
         self.max_batch = int(max_batch)
         self.max_batch_bytes = int(max_batch_bytes)
         self._held = None  # the request that did not fit the previous batch
+        self._last_batch = 0  # size of the previous batch: the collection window opens only after a batch > 1
         self._q: queue.SimpleQueue = queue.SimpleQueue()
         self._thread: threading.Thread | None = None
         self._start_lock = threading.Lock()
@@ -143,7 +145,9 @@ class QueryCoalescer:
             batch = [first]
             nbytes = _size(first[0])
             stop = False
-            deadline = time.monotonic() + self.window_s
+            # low load (the previous batch was one request): dispatch what is queued now, no wait for company
+            window = self.window_s if self._last_batch > 1 else 0.0
+            deadline = time.monotonic() + window
             while len(batch) < self.max_batch:
                 try:
                     item = self._q.get_nowait()
@@ -171,6 +175,7 @@ class QueryCoalescer:
                 return
 
     def _dispatch(self, batch) -> None:
+        self._last_batch = len(batch)
         self.batches.append(len(batch))
         del self.batches[:-1024]
         live = [(p, f) for p, f in batch if f.set_running_or_notify_cancel()]

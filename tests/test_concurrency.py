@@ -69,3 +69,33 @@ def test_coalescer_lone_request_latency():
         c("x")
     assert (time.perf_counter() - t) / 50 < 0.01
     c.close()
+
+
+def test_coalescer_window_opens_only_under_load():
+    """A lone request (the previous batch was one request) is dispatched at once, even with a long window; after a
+    batch of several requests the window collects the next ones."""
+    import threading
+
+    seen = []
+    gate = threading.Event()
+
+    def run(batch):
+        seen.append(len(batch))
+        gate.wait(5)
+        return batch
+
+    c = QueryCoalescer(run, window_s=0.2, max_batch=64)
+    gate.set()
+    t = time.perf_counter()
+    for _ in range(5):
+        c("x")
+    assert (time.perf_counter() - t) / 5 < 0.05  # no 0.2 s window per lone request
+    gate.clear()
+    first = c.submit("a")  # occupies the dispatcher
+    time.sleep(0.05)
+    futs = [c.submit(i) for i in range(8)]  # queue up behind it
+    gate.set()
+    first.result(5)
+    assert [f.result(5) for f in futs] == list(range(8))
+    assert seen[-1] == 8  # taken together
+    c.close()
