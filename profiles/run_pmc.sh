@@ -4,4 +4,4 @@ set -e
 OUTD=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/$OUTD
-timeout -k 10 300 rocprofv3 --pmc "$@" -T -d gpurun_out/$OUTD -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog > gpurun_out/$OUTD/log 2>&1
+timeout -k 10 300 rocprofv3 --pmc "$@" -T -d gpurun_out/$OUTD -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-service --no-stream > gpurun_out/$OUTD/log 2>&1
