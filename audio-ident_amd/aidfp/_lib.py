@@ -111,6 +111,7 @@ SIGNATURES = [
     ("aid_match_stats", ctypes.c_int, [P, P, I32, I32]),
     ("aid_index_export", ctypes.c_int, [P, P, P, P, I64, I64, I32]),
     ("aid_index_checksum", ctypes.c_int, [P, I64, I64, P]),
+    ("aid_index_csr_export", ctypes.c_int, [P, P, I64, P, I64, P]),
     ("aid_comm_id", ctypes.c_int, [P]),
     ("aid_comm_create", ctypes.c_int, [P, P, I32, I32, P]),
     ("aid_comm_destroy", None, [P]),

@@ -439,6 +439,17 @@ class Engine:
         check(self._lib.aid_index_checksum(self._h, int(first), int(count), ctypes.byref(out)))
         return int(out.value)
 
+    def index_csr(self, offsets: bool = True) -> tuple[np.ndarray | None, np.ndarray]:
+        """aid_index_csr_export: the finalized CSR as (offsets u32 [2^26 + 1] or None, posts u64 [n])."""
+        n = ctypes.c_int64(0)
+        check(self._lib.aid_index_csr_export(self._h, None, 0, None, 0, ctypes.byref(n)))
+        posts = np.empty(int(n.value), np.uint64)
+        offs = np.empty((1 << 26) + 1, np.uint32) if offsets else None
+        check(self._lib.aid_index_csr_export(self._h, None if offs is None else offs.ctypes.data_as(ctypes.c_void_p),
+                                             0 if offs is None else len(offs),
+                                             posts.ctypes.data_as(ctypes.c_void_p), len(posts), ctypes.byref(n)))
+        return offs, posts
+
     def index_export_device(self, hash_ptr: int, track_ptr: int, t_ptr: int, first: int, count: int) -> None:
         check(self._lib.aid_index_export(self._h, ctypes.c_void_p(hash_ptr), ctypes.c_void_p(track_ptr),
                                          ctypes.c_void_p(t_ptr), first, count, AID_PCM_DEVICE))

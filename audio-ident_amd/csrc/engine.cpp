@@ -54,7 +54,7 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
                                    uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
                                    uint32_t *scratch, uint32_t *E, uint32_t *offsets, unsigned long long *nz,
-                                   uint64_t **vals_out, uint16_t *sig, hipStream_t s);
+                                   uint64_t **vals_out, uint16_t *sig, int rank_mode, hipStream_t s);
 void launch_make_sig(const uint64_t *post, int64_t n, uint16_t *sig, hipStream_t s);
 void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
                     uint32_t n_tracks, uint32_t *cnt, uint32_t *off, uint32_t *tmp, uint32_t *oh, uint32_t *otrack,
@@ -178,6 +178,8 @@ struct aid_engine {
     DevBuf<uint8_t> srt_tmp;          // K4 rocPRIM build (A/B): its temporary storage
     DevBuf<uint32_t> srt_scratch;     // K4 radix build: per-tile digit counts, their scan, scan temporary
     int k4_mode = 2;                  // aid_engine_force K4_BUILD: 2 radix sort (default), 1 rocPRIM sort, 0 atomic
+    int k4_rank = 0;                  // radix sort's in-wave rank: 0 one LDS atomic per posting where the device
+                                      // serves same-address lanes in order (else ballots), 1 ballots (K4_BUILD 4)
     bool index_built = false, index_dirty = true;
     int64_t n_indexed = 0;
     int64_t n_buckets_used = 0;
@@ -530,8 +532,10 @@ int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
             e->desc_dev_for_key = nullptr;  // strip bases change: rebuild the descriptors
             return AID_OK;
         case AID_FORCE_K4_BUILD:
-            if (value < 0 || value > 3) return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 radix, 2 atomic, 3 rocPRIM");
+            if (value < 0 || value > 4)
+                return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 radix, 2 atomic, 3 rocPRIM, 4 radix with ballot ranks");
             e->k4_mode = value == 2 ? 0 : value == 3 ? 1 : 2;
+            e->k4_rank = value == 4 ? 1 : 0;
             e->index_dirty = true;
             return AID_OK;
         case AID_FORCE_EXCHANGE_FAIL:
@@ -1403,7 +1407,7 @@ static int finalize_locked(aid_engine *e) {
                                             any_removed ? e->tomb.p : nullptr, e->n_tracks,
                                             e->srt_k0.p, e->srt_k1.p, e->srt_v.p, e->idx_post.p, e->srt_tmp.p, tb,
                                             rocprim_ab, e->srt_scratch.p, e->idx_cnt.p, e->idx_off.p, e->nz.p, &sorted,
-                                            e->idx_sig.p, s));
+                                            e->idx_sig.p, e->k4_rank, s));
             if (sorted == e->srt_v.p) std::swap(e->srt_v, e->idx_post);  // the CSR's post array is where the sort ended
         }
     } else {
@@ -1755,6 +1759,27 @@ int aid_index_checksum(aid_engine *e, int64_t first, int64_t count, uint64_t *ou
     HIP_TRY(hipMemcpyAsync(&v, e->chk.p, sizeof(v), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *out = (uint64_t)v;
+    return AID_OK;
+}
+
+int aid_index_csr_export(aid_engine *e, uint32_t *offsets, int64_t n_offsets, uint64_t *posts, int64_t cap,
+                         int64_t *n_out) {
+    if (!e || !n_out || n_offsets < 0 || cap < 0 || (!offsets && n_offsets > 0) || (!posts && cap > 0))
+        return fail(AID_ERR_INVALID, "aid_index_csr_export: bad argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (!e->index_built || e->index_dirty) return fail(AID_ERR_STATE, "aid_index_csr_export: the index is not finalized");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    const int64_t K = (int64_t)index_keys() + 1;
+    *n_out = e->n_indexed;
+    if (offsets && n_offsets > 0) {
+        if (n_offsets < K) return fail(AID_ERR_INVALID, "aid_index_csr_export: offsets need 2^26 + 1 entries");
+        HIP_TRY(hipMemcpy(offsets, e->idx_off.p, K * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    if (posts && cap > 0) {
+        const int64_t n = std::min<int64_t>(cap, e->n_indexed);
+        if (n > 0) HIP_TRY(hipMemcpy(posts, e->idx_post.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    }
     return AID_OK;
 }
 

@@ -16,10 +16,13 @@
 //            group of kColTiles tiles, a column scan of those with the digit totals' exclusive scan, then
 //            each group's running column prefix (every read and write a contiguous row);
 //   scatter  a workgroup of 4 waves loads its tile (wave w: items w*1024 .. +1023, 64 consecutive per
-//            load), ranks every item stably inside the tile (ballot match per 64-item slot, wave-private
-//            running digit counters by LDS atomics issued back to back, cross-wave offsets), stages the tile
-//            in LDS in sorted order (48 KB: two workgroups per CU overlap one's loads with the other's
-//            ranking) and writes it out in runs of consecutive positions per digit.
+//            load), ranks every item stably inside the tile (one LDS atomic per item on a wave-private
+//            digit counter, slot by slot: the wave's atomics execute in issue order and, as checked on the
+//            device before the first build, same-counter lanes of one atomic are served in lane order; where
+//            that check fails, a ballot match per 64-item slot and one atomic per digit group), then
+//            cross-wave offsets, stages the tile in LDS in sorted order (52 KB with the counters in the key
+//            area: three workgroups per CU overlap loads with ranking) and writes it out in runs of
+//            consecutive positions per digit.
 // Pass 1 reads the SoA postings (hash, track, t) itself (key generation fused in; the tombstones and the track
 // column for the count only when a track is removed); pass 3 writes the values straight into the CSR's post array
 // and, instead of a sorted key array, the CSR's run ends: at the last posting i of each key's run,
@@ -30,6 +33,8 @@
 // Tiles are dealt XCD-contiguously (xcd_tile): adjacent tiles' partial lines complete in one L2.
 // Bytes per posting: 4 (count 1) + 24 (scatter 1) + 2 x 4 (counts 2, 3) + 24 (scatter 2) + 20 (scatter 3) = 80,
 // plus ~4 per distinct key (E) and the 2 KB of counts per tile per pass.
+#include <atomic>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "aidfp_device.h"
@@ -45,6 +50,16 @@ constexpr int kSortPasses = 3;
 #endif
 constexpr int kSortThreads = AID_K4_THREADS;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
+// AID_K4_DIAG (timing-only variant builds, probes/run_r05m.sh; wrong output): 2 = each scatter writes its sorted tile
+// back in place (sequential writes), 3 = no global writes
+#ifndef AID_K4_DIAG
+#define AID_K4_DIAG 0
+#endif
+// AID_K4_LDS3 = 1: the scatter's per-wave counters share the key staging area (52 KB, three workgroups per CU);
+// 0 (A/B builds only): separate counters (61 KB, two per CU)
+#ifndef AID_K4_LDS3
+#define AID_K4_LDS3 1
+#endif
 #ifndef AID_K4_SLOTS
 #define AID_K4_SLOTS 16  // A/B builds only (build_ext variant defines)
 #endif
@@ -218,8 +233,9 @@ static void digit_starts(const uint32_t *counts, int64_t tiles, uint32_t *offs, 
                        (const uint32_t *)goff, (const uint32_t *)base, offs);
 }
 
-template <bool FIRST, bool LAST, bool TOMB = false>
-__global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
+// ARANK: the stable in-wave rank by one LDS atomic per posting (lds_lane_order_ok() must hold), else by ballots
+template <bool FIRST, bool LAST, bool TOMB = false, bool ARANK = false>
+__global__ __launch_bounds__(kSortThreads, AID_K4_LDS3 ? 3 : 2) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
                                                                 const uint64_t *__restrict__ vals_in,
                                                                 const uint32_t *__restrict__ ptrack,
                                                                 const uint32_t *__restrict__ pt,
@@ -230,9 +246,17 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
                                                                 uint64_t *__restrict__ vals_out,
                                                                 uint32_t *__restrict__ E,
                                                                 uint16_t *__restrict__ sig_out) {
+#if AID_K4_LDS3
+    // the per-wave counters live in the front of the key staging area (52 KB per workgroup: three per CU): every
+    // posting's staging position is taken from them before the barrier that precedes the staging
+    static_assert(kSortWaves * kDigits <= kTile, "counters fit the key staging area");
     __shared__ uint32_t s_key[kTile];
-    __shared__ uint64_t s_val[kTile];
+    uint32_t(*cnt)[kDigits] = reinterpret_cast<uint32_t(*)[kDigits]>(s_key);
+#else
+    __shared__ uint32_t s_key[kTile];
     __shared__ uint32_t cnt[kSortWaves][kDigits];  // running per-wave counters, then cross-wave offsets
+#endif
+    __shared__ uint64_t s_val[kTile];
     __shared__ uint32_t t_start[kDigits];          // first local position of each digit in the tile
     __shared__ uint32_t g_start[kDigits];          // global position of (digit, tile)
     __shared__ uint32_t wsum[kSortWaves];
@@ -276,21 +300,34 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
     // group adds the group's size to the wave's running counter and gets the count before it (LDS atomics of
     // one wave are executed in order, so slot s sees slots 0..s-1); the 16 slots' atomics issue back to back,
     // then each lane takes its leader's value (a cross-lane read) and adds its place in the group
-    uint32_t rank[kSlots], old[kSlots];
-    int lead[kSlots];
+    uint32_t rank[kSlots];
+    if constexpr (ARANK) {
+        // one LDS atomic per posting: the old value is the number of earlier postings of the wave with the same
+        // digit, given that a wave's LDS atomics execute in issue order (slot by slot) and that the lanes of one
+        // ds_add_rtn that hit the same counter are served in ascending lane order (checked on the device before
+        // this path is taken: lds_lane_order_ok)
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
-        const uint64_t valid = valid_lanes(base + s * 64, n);
-        const uint32_t d = (key[s] >> shift) & (kDigits - 1);
-        const uint64_t m = match_digit(d, valid);
-        const uint64_t mine = m | (1ull << lane);  // an invalid lane leads its own (empty) group
-        lead[s] = __ffsll((unsigned long long)mine) - 1;
-        rank[s] = (uint32_t)__popcll(m & lanemask_lt(lane));
-        old[s] = 0;
-        if (((valid >> lane) & 1) && lead[s] == lane) old[s] = atomicAdd(&cnt[w][d], (uint32_t)__popcll(m));
+        for (int s = 0; s < kSlots; ++s) {
+            const uint32_t d = (key[s] >> shift) & (kDigits - 1);
+            rank[s] = base + s * 64 + lane < n ? atomicAdd(&cnt[w][d], 1u) : 0u;
+        }
+    } else {
+        uint32_t old[kSlots];
+        int lead[kSlots];
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            const uint64_t valid = valid_lanes(base + s * 64, n);
+            const uint32_t d = (key[s] >> shift) & (kDigits - 1);
+            const uint64_t m = match_digit(d, valid);
+            const uint64_t mine = m | (1ull << lane);  // an invalid lane leads its own (empty) group
+            lead[s] = __ffsll((unsigned long long)mine) - 1;
+            rank[s] = (uint32_t)__popcll(m & lanemask_lt(lane));
+            old[s] = 0;
+            if (((valid >> lane) & 1) && lead[s] == lane) old[s] = atomicAdd(&cnt[w][d], (uint32_t)__popcll(m));
+        }
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) rank[s] += (uint32_t)__shfl((int)old[s], lead[s], 64);
     }
-#pragma unroll
-    for (int s = 0; s < kSlots; ++s) rank[s] += (uint32_t)__shfl((int)old[s], lead[s], 64);
     __syncthreads();
     // thread = 2 consecutive digits: cross-wave exclusive offsets (in place) and the tile's digit totals, then
     // the exclusive scan of the totals over the digits (the thread's pair, wave shuffles, wave totals)
@@ -327,16 +364,22 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
         start += tot[j];
     }
     __syncthreads();
-    // stage the tile in LDS in sorted (digit, item) order
+    // stage the tile in LDS in sorted (digit, item) order: every posting's position first (a permutation of [0, tile
+    // items); kTile = not staged), then, once no wave reads the counters any more, the staging over them
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
-        if (base + s * 64 + lane < n) {
-            const uint32_t d = (key[s] >> shift) & (kDigits - 1);
-            const uint32_t pos = t_start[d] + cnt[w][d] + rank[s];  // a permutation of [0, tile items)
-            if (pos < kTile) {
-                s_key[pos] = key[s];
-                s_val[pos] = val[s];
-            }
+        const uint32_t d = (key[s] >> shift) & (kDigits - 1);
+        rank[s] = base + s * 64 + lane < n ? t_start[d] + cnt[w][d] + rank[s] : (uint32_t)kTile;
+    }
+#if AID_K4_LDS3
+    __syncthreads();
+#endif
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        const uint32_t pos = rank[s];
+        if (pos < kTile) {
+            s_key[pos] = key[s];
+            s_val[pos] = val[s];
         }
     }
     __syncthreads();
@@ -346,8 +389,15 @@ __global__ __launch_bounds__(kSortThreads, 2) void k_radix_scatter(const uint32_
     for (int i = tid; i < m; i += kSortThreads) {
         const uint32_t k = s_key[i];
         const uint32_t d = (k >> shift) & (kDigits - 1);
+#if AID_K4_DIAG == 2
+        const int64_t dst = tile0 + i;  // timing-only: the sorted tile written back in place (sequential writes)
+#else
         const int64_t dst = (int64_t)g_start[d] + (i - (int)t_start[d]);
+#endif
         if (dst >= n) continue;  // cannot happen for consistent counts; never write out of bounds
+#if AID_K4_DIAG == 3
+        if (k != 0xFFFFFFFEu) continue;  // timing-only: no global writes (a key that never occurs)
+#endif
         if (LAST) {
             // the run ends of the CSR, from the sorted tile itself (no key array is written): inside a digit run
             // the tile's items are in full key order (stable passes), so a key change there is the key's last
@@ -482,6 +532,55 @@ static void scan8(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, h
     }
 }
 
+// ---- the device property ARANK relies on, checked once per device before the first build that would use it ----
+// Every wave of 64 workgroups adds 1 to one of its own 512 LDS counters per lane, 64 times, with digit patterns from
+// all-distinct to all-equal; for every pair of lanes l < l' that hit the same counter in one instruction, l' must get
+// the larger old value. *viol counts the pairs that do not (0 on gfx950: profiles/r05n_lds_atomic_order.json)
+__global__ __launch_bounds__(256) void k_lds_lane_order(uint32_t *__restrict__ viol) {
+    __shared__ uint32_t cnt[4][kDigits];
+    __shared__ uint32_t ret[4][64];
+    __shared__ uint32_t dig[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 4 * kDigits; i += 256) (&cnt[0][0])[i] = 0u;
+    __syncthreads();
+    uint32_t v = 0;
+    for (int r = 0; r < 64; ++r) {
+        uint32_t x = (blockIdx.x * 0x9E3779B9u) ^ (r * 0x85EBCA6Bu) ^ (w * 0xC2B2AE35u) ^ (lane * 0x27D4EB2Fu);
+        x ^= x >> 15;
+        x *= 0x2C1B3C6Du;
+        x ^= x >> 12;
+        const int p = r & 3;
+        const uint32_t d = p == 0 ? x & (kDigits - 1) : p == 1 ? x & 3u : p == 2 ? 5u : (x & 1u) ? (x >> 1) & 7u : 300u;
+        const uint32_t old = atomicAdd(&cnt[w][d], 1u);
+        ret[w][lane] = old;
+        dig[w][lane] = d;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int l2 = lane + 1; l2 < 64; ++l2) v += (dig[w][l2] == d && ret[w][l2] <= old) ? 1u : 0u;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (v) atomicAdd(viol, v);
+}
+
+// 1 = ds_add_rtn serves same-address lanes in ascending lane order on this device, 0 = not, <0 = the check failed
+static int lds_lane_order_ok(uint32_t *dev_word, hipStream_t s) {
+    static std::atomic<int> state[64];  // per device: 0 unknown, 1 ok, 2 not ok
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    const int st = state[dev].load();
+    if (st) return st == 1 ? 1 : 0;
+    if (hipMemsetAsync(dev_word, 0, sizeof(uint32_t), s) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_lds_lane_order, dim3(64), dim3(256), 0, s, dev_word);
+    uint32_t viol = 1;
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(&viol, dev_word, sizeof(viol), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    state[dev].store(viol == 0 ? 1 : 2);
+    return viol == 0 ? 1 : 0;
+}
+
 // ---- rocPRIM reference build (A/B only) ----
 __global__ void k_sort_keys(const uint32_t *__restrict__ ph, const uint32_t *__restrict__ ptrack,
                             const uint32_t *__restrict__ pt, int64_t n, const uint8_t *__restrict__ tomb,
@@ -514,6 +613,45 @@ size_t index_sort_temp_bytes(int64_t n) {
     return bytes;
 }
 
+// the three passes of the hand-written sort: SoA postings -> (keys1, vals1) -> (keys0, vals0) -> the CSR's values in
+// vals1, its run ends in E and the K5 signatures in sig
+template <bool ARANK>
+static void radix_passes(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n, const uint8_t *tomb,
+                         uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1, uint64_t *vals0, uint64_t *vals1,
+                         uint32_t *counts, uint32_t *offs, uint32_t *stmp, uint32_t *E, uint16_t *sig, int64_t tiles,
+                         hipStream_t s) {
+    // pass 1: SoA postings -> (keys1, vals1); pass 2: -> (keys0, vals0); pass 3: -> (keys1, vals1)
+    const dim3 g((unsigned)tiles), b(kSortThreads);
+    if (tomb) {
+        timed_launch(k_radix_count<true, true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
+        digit_starts(counts, tiles, offs, stmp, s);
+        timed_launch(k_radix_scatter<true, false, true, ARANK>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
+                     tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr,
+                     (uint16_t *)nullptr);
+    } else {
+        timed_launch(k_radix_count<true, false>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
+        digit_starts(counts, tiles, offs, stmp, s);
+        timed_launch(k_radix_scatter<true, false, false, ARANK>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
+                     tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr,
+                     (uint16_t *)nullptr);
+    }
+    timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
+                 (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
+    digit_starts(counts, tiles, offs, stmp, s);
+    timed_launch(k_radix_scatter<false, false, false, ARANK>, g, b, 0, s, (const uint32_t *)keys1,
+                 (const uint64_t *)vals1, (const uint32_t *)nullptr, (const uint32_t *)nullptr,
+                 (const uint8_t *)nullptr, 0u, n, kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0,
+                 (uint32_t *)nullptr, (uint16_t *)nullptr);
+    timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys0, (const uint32_t *)nullptr,
+                 (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, counts, tiles);
+    digit_starts(counts, tiles, offs, stmp, s);
+    timed_launch(k_radix_scatter<false, true, false, ARANK>, g, b, 0, s, (const uint32_t *)keys0,
+                 (const uint64_t *)vals0, (const uint32_t *)nullptr, (const uint32_t *)nullptr,
+                 (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, (const uint32_t *)offs, tiles,
+                 (uint32_t *)nullptr,
+                 vals1, E, sig);
+}
+
 // keys0/keys1: n u32 each; vals0/vals1: n u64 each (the sorted values end in *vals_out, one of the two).
 // E (2^26 + 1 u32, zeroed by the caller) receives the run ends, offsets the CSR offsets, *nz (zeroed) the
 // number of live keys. use_rocprim: the A/B reference (temp/temp_bytes its storage); `scratch` holds
@@ -522,7 +660,7 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
                                    uint64_t *vals0, uint64_t *vals1, void *temp, size_t temp_bytes, bool use_rocprim,
                                    uint32_t *scratch, uint32_t *E, uint32_t *offsets, unsigned long long *nz,
-                                   uint64_t **vals_out, uint16_t *sig, hipStream_t s) {
+                                   uint64_t **vals_out, uint16_t *sig, int rank_mode, hipStream_t s) {
     *vals_out = vals0;
     const int64_t K = (int64_t)(1u << 26) + 1;
     const int64_t tiles = radix_tiles(n);
@@ -542,33 +680,19 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
         *vals_out = v.current();
     } else if (n > 0) {
         uint32_t *counts = scratch, *offs = scratch + c;
-        // pass 1: SoA postings -> (keys1, vals1); pass 2: -> (keys0, vals0); pass 3: -> (keys1, vals1)
-        const dim3 g((unsigned)tiles), b(kSortThreads);
-        if (tomb) {
-            timed_launch(k_radix_count<true, true>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
-            digit_starts(counts, tiles, offs, stmp, s);
-            timed_launch(k_radix_scatter<true, false, true>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
-                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr,
-                         (uint16_t *)nullptr);
-        } else {
-            timed_launch(k_radix_count<true, false>, g, b, 0, s, ph, ptrack, tomb, n_tracks, n, 0, counts, tiles);
-            digit_starts(counts, tiles, offs, stmp, s);
-            timed_launch(k_radix_scatter<true, false, false>, g, b, 0, s, ph, (const uint64_t *)nullptr, ptrack, pt,
-                         tomb, n_tracks, n, 0, (const uint32_t *)offs, tiles, keys1, vals1, (uint32_t *)nullptr,
-                         (uint16_t *)nullptr);
+        // rank_mode 0: the one-atomic rank where the device serves same-address LDS lanes in order, 1: ballots
+        bool arank = false;
+        if (rank_mode == 0) {
+            const int ok = lds_lane_order_ok(scratch + radix_scratch_u32(n) - 1, s);
+            if (ok < 0) return hipErrorUnknown;
+            arank = ok == 1;
         }
-        timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys1, (const uint32_t *)nullptr,
-                     (const uint8_t *)nullptr, 0u, n, kDigitBits, counts, tiles);
-        digit_starts(counts, tiles, offs, stmp, s);
-        timed_launch(k_radix_scatter<false, false>, g, b, 0, s, (const uint32_t *)keys1, (const uint64_t *)vals1,
-                     (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
-                     kDigitBits, (const uint32_t *)offs, tiles, keys0, vals0, (uint32_t *)nullptr, (uint16_t *)nullptr);
-        timed_launch(k_radix_count<false>, g, b, 0, s, (const uint32_t *)keys0, (const uint32_t *)nullptr,
-                     (const uint8_t *)nullptr, 0u, n, 2 * kDigitBits, counts, tiles);
-        digit_starts(counts, tiles, offs, stmp, s);
-        timed_launch(k_radix_scatter<false, true>, g, b, 0, s, (const uint32_t *)keys0, (const uint64_t *)vals0,
-                     (const uint32_t *)nullptr, (const uint32_t *)nullptr, (const uint8_t *)nullptr, 0u, n,
-                     2 * kDigitBits, (const uint32_t *)offs, tiles, (uint32_t *)nullptr, vals1, E, sig);
+        if (arank)
+            radix_passes<true>(ph, ptrack, pt, n, tomb, n_tracks, keys0, keys1, vals0, vals1, counts, offs, stmp, E, sig,
+                               tiles, s);
+        else
+            radix_passes<false>(ph, ptrack, pt, n, tomb, n_tracks, keys0, keys1, vals0, vals1, counts, offs, stmp, E, sig,
+                                tiles, s);
         *vals_out = vals1;
     }
     if (n > 0 && sorted_keys) {  // rocPRIM: run ends from its sorted keys, the signatures from its values

@@ -98,7 +98,8 @@ int aid_engine_config(const aid_engine *e, aid_config *out);
 #define AID_FORCE_K5_PARTS 2       /* 0 by vote count, else 1, 2 or 4 key partitions per query (K5a) */
 #define AID_FORCE_K5_BATCH 3       /* 0 default (2048), else global-path queries per launch */
 #define AID_FORCE_K2_STRIPS_X100 4 /* 0 adaptive, else 100 x K2 strips per resident workgroup slot */
-#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B) */
+#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B),
+                                      4 radix sort with the ballot-matched in-wave rank (A/B of the one-atomic rank) */
 #define AID_FORCE_EXCHANGE_FAIL 6  /* 1: the next index exchange's pack (aid_index_pack, or the prepare step of
                                       aid_index_allgather) fails with AID_ERR_NOMEM, once (rank-failure tests) */
 #define AID_FORCE_LANE_GATHER 7    /* 1: aid_exact_lane copies its sub-windows to a staging buffer before K1 instead
@@ -208,6 +209,13 @@ int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t
    i counted from `first`. After the catalog exchange every rank compares its replica's checksum with the others'
    (the sequential ingest it replaces, app/ingest/pipeline.py:294-310, had one LMDB and nothing to compare). */
 int aid_index_checksum(aid_engine *e, int64_t first, int64_t count, uint64_t *out);
+/* The built CSR to host memory (tests and tools; the index must be finalized): offsets (n_offsets >= 2^26 + 1, or
+   NULL) = the start of each bucket key's postings (offsets[k]..offsets[k+1]), posts (up to cap, or NULL) = the
+   postings (track | t << 32) in bucket-key order, each bucket in arrival order (K4 is a stable sort); *n_out = the
+   postings in the CSR (removed tracks' postings dropped). Replaces reading the LMDB that `olaf_c store` writes
+   (audio-ident-service/app/audio/fingerprint.py:117-125). */
+int aid_index_csr_export(aid_engine *e, uint32_t *offsets, int64_t n_offsets, uint64_t *posts, int64_t cap,
+                         int64_t *n_out);
 /* ---- PCM front-end (spec/FPSPEC.md 8) ----
  * Replaces ffmpeg `-ac 1 -ar <rate>` (audio-ident-service/app/audio/decode.py:41-60): optional
  * stereo downmix ((L+R)*0.5f) + rational polyphase resampling sr_in -> sr_out (scipy

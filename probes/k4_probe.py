@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--tracks", type=int, default=100000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="radix,rocprim,atomic,radix_again",
-                    help="builds to time, of radix, rocprim, atomic, radix_again (AIDFP_LIB picks an A/B library)")
+                    help="builds to time, of radix, rocprim, atomic, radix_again, radix_ballot (the ballot-matched "
+                         "in-wave rank) (AIDFP_LIB picks an A/B library)")
     args = ap.parse_args()
     import torch
 
@@ -38,7 +39,7 @@ def main():
 
     out = {"postings": st.postings_total, "library": os.environ.get("AIDFP_LIB", "product")}
     ref = None
-    modes = [m for m in (("radix", 1), ("rocprim", 3), ("atomic", 2), ("radix_again", 1))
+    modes = [m for m in (("radix", 1), ("rocprim", 3), ("atomic", 2), ("radix_again", 1), ("radix_ballot", 4))
              if m[0] in args.modes.split(",")]
     for name, mode in modes:
         eng.force("k4_build", mode)

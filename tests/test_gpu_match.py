@@ -320,3 +320,60 @@ def test_sort_build_many_column_groups(removed):
     gone = {int(tracks[i]) for i in pick[:5]} if removed else set()
     assert sum(h == int(tracks[i]) for h, i in zip(hits, pick) if int(tracks[i]) not in gone) >= 40
     assert not any(h in gone for h in hits if h is not None)
+
+
+def _bucket_key_np(h):
+    """Host mirror of aidfp_layout.h bucket_key (the CSR's key permutation of the 26 hash bits)."""
+    h = h.astype(np.uint32)
+    return ((((h >> 22) & 0xFF) << 18) | ((h >> 30) << 16) | (((h >> 12) & 0x7F) << 9) | (((h >> 19) & 0x7) << 6) |
+            (h & 0x3F)).astype(np.uint32)
+
+
+def _csr_mirror(post, removed):
+    """The CSR K4 must build from stored postings [n, 3] (hash, track, t): live postings stably sorted by bucket key
+    (a bucket keeps arrival order), values track | t << 32, offsets[k] = live postings with key < k."""
+    live = ~np.isin(post[:, 1], np.asarray(list(removed), dtype=np.uint32))
+    p = post[live]
+    keys = _bucket_key_np(p[:, 0])
+    order = np.argsort(keys, kind="stable")
+    posts = p[order, 1].astype(np.uint64) | (p[order, 2].astype(np.uint64) << np.uint64(32))
+    counts = np.bincount(keys, minlength=1 << 26)
+    offs = np.zeros((1 << 26) + 1, np.uint32)
+    offs[1:] = np.cumsum(counts).astype(np.uint32)
+    return offs, posts
+
+
+@pytest.mark.parametrize("mode", ["sort", "ballot", "rocprim"])
+def test_csr_layout_equals_stable_mirror(mode):
+    """The built CSR itself, not only the rows queries read from it: the hand-written radix build (its default rank,
+    one LDS atomic per posting; and the ballot-matched rank, force 4), and rocPRIM's, the A/B reference, lay out
+    exactly the stable key sort of the stored postings (arrival order inside a bucket), with
+    removed tracks' postings dropped and offsets equal to the key histogram's prefix sums; over more than one K4
+    tile and column group (~1.4 M postings)."""
+    import torch
+
+    n = SR * 12
+    tracks = np.arange(600, dtype=np.uint32) * 5 + 2
+    removed = {int(tracks[3]), int(tracks[300]), int(tracks[599])}
+    eng = Engine(SR)
+    try:
+        eng.force("k4_build", {"sort": 1, "ballot": 4, "rocprim": 3}[mode])
+        pcm = torch.empty(200 * n, dtype=torch.float32, device="cuda")
+        for b0 in range(0, len(tracks), 200):
+            tr = tracks[b0:b0 + 200]
+            eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n)
+            eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n)
+            eng.index_add_extracted(tr)
+        for t in sorted(removed):
+            eng.index_remove(t)
+        eng.index_finalize()
+        post = eng.index_export()
+        offs, posts = eng.index_csr()
+    finally:
+        eng.close()
+    assert len(post) > 256 * 4096
+    ref_offs, ref_posts = _csr_mirror(post, removed)
+    assert len(posts) == len(ref_posts)
+    bad = np.flatnonzero(posts != ref_posts)
+    assert len(bad) == 0, f"{len(bad)} CSR postings out of place, first at {bad[:5]}"
+    assert np.array_equal(offs, ref_offs)
