@@ -208,7 +208,7 @@ def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
     audio_mt = passes * sample.shape[0] * sample.shape[1] / SR
     audio_1 = one.shape[0] * one.shape[1] / SR
     np_leg = numpy_baseline(sample[:16], threads)
-    cat = catalog_cpu_estimate(O, ref, audio_mt / dt_mt, threads)
+    cat = catalog_cpu_estimate(O, ref, audio_mt / dt_mt, threads, batch_s=sample.shape[0] * sample.shape[1] / SR)
     return ref, {
         "value": round(audio_mt / dt_mt, 1),
         "unit": "audio-s/s",
@@ -226,11 +226,12 @@ def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
     }
 
 
-def catalog_cpu_estimate(O, ref: list, extract_rate: float, threads: int, tracks: int = 100000,
-                         track_s: float = 30.0, postings: int = 911675195) -> dict:
+def catalog_cpu_estimate(O, ref: list, extract_rate: float, threads: int, batch_s: float, tracks: int = 100000,
+                         track_s: float = 30.0) -> dict:
     """Config 3 on the host (sub-sampled, extrapolated, labelled): the catalog's extraction at the
     multi-thread oracle rate measured above, plus the index build as the oracle's sort (fp_index_sort, one thread)
-    of the batch's own postings, scaled n log n to the catalog's posting count (bench.py catalog leg)."""
+    of the batch's own postings, scaled n log n to the catalog's posting count (the batch's postings per audio
+    second times the catalog's audio: ~580 M for generator v2, as the bench's catalog leg holds)."""
     p = np.concatenate([np.stack([(r & np.uint64(0xFFFFFFFF)).astype(np.uint32), np.full(len(r), c, np.uint32),
                                   (r >> np.uint64(32)).astype(np.uint32)], axis=1) for c, r in enumerate(ref)])
     p = np.ascontiguousarray(p)
@@ -238,8 +239,9 @@ def catalog_cpu_estimate(O, ref: list, extract_rate: float, threads: int, tracks
     O.lib().fp_index_sort(O._ptr(p), len(p))
     ts = time.perf_counter() - t
     n = len(p)
-    sort_s = ts * (postings / n) * (np.log2(postings) / np.log2(max(n, 2)))
     audio = tracks * track_s
+    postings = int(round(n * audio / batch_s))
+    sort_s = ts * (postings / n) * (np.log2(postings) / np.log2(max(n, 2)))
     extract_s = audio / extract_rate
     return {"value": float(round(audio / (extract_s + sort_s), 1)), "unit": "audio-s/s", "extrapolated": True,
             "sample": f"extraction at the {threads}-thread oracle rate above ({extract_s:.0f} s for {tracks} x "
