@@ -377,3 +377,24 @@ def test_csr_layout_equals_stable_mirror(mode):
     bad = np.flatnonzero(posts != ref_posts)
     assert len(bad) == 0, f"{len(bad)} CSR postings out of place, first at {bad[:5]}"
     assert np.array_equal(offs, ref_offs)
+
+
+def test_csr_export_needs_a_finalized_index():
+    """aid_index_csr_export refuses a stale index (AID_ERR_STATE) and returns an empty CSR for an empty one."""
+    from aidfp._lib import AID_ERR_STATE, EngineError
+
+    eng = Engine(SR)
+    try:
+        eng.index_finalize()
+        offs, posts = eng.index_csr()
+        assert len(posts) == 0 and offs[0] == 0 and offs[-1] == 0
+        rec = O.fingerprint(synth.synth(3, 0, 5 * SR, SR), HOP)
+        eng.index_add_records(3, rec)
+        with pytest.raises(EngineError) as e:
+            eng.index_csr(offsets=False)
+        assert e.value.code == AID_ERR_STATE
+        eng.index_finalize()
+        _, posts = eng.index_csr(offsets=False)
+        assert len(posts) == len(rec)
+    finally:
+        eng.close()
