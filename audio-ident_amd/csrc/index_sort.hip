@@ -50,16 +50,6 @@ constexpr int kSortPasses = 3;
 #endif
 constexpr int kSortThreads = AID_K4_THREADS;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
-// AID_K4_DIAG (timing-only variant builds, probes/run_r05m.sh; wrong output): 2 = each scatter writes its sorted tile
-// back in place (sequential writes), 3 = no global writes
-#ifndef AID_K4_DIAG
-#define AID_K4_DIAG 0
-#endif
-// AID_K4_LDS3 = 1: the scatter's per-wave counters share the key staging area (52 KB, three workgroups per CU);
-// 0 (A/B builds only): separate counters (61 KB, two per CU)
-#ifndef AID_K4_LDS3
-#define AID_K4_LDS3 1
-#endif
 #ifndef AID_K4_SLOTS
 #define AID_K4_SLOTS 16  // A/B builds only (build_ext variant defines)
 #endif
@@ -235,7 +225,7 @@ static void digit_starts(const uint32_t *counts, int64_t tiles, uint32_t *offs, 
 
 // ARANK: the stable in-wave rank by one LDS atomic per posting (lds_lane_order_ok() must hold), else by ballots
 template <bool FIRST, bool LAST, bool TOMB = false, bool ARANK = false>
-__global__ __launch_bounds__(kSortThreads, AID_K4_LDS3 ? 3 : 2) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
+__global__ __launch_bounds__(kSortThreads, 3) void k_radix_scatter(const uint32_t *__restrict__ keys_in,
                                                                 const uint64_t *__restrict__ vals_in,
                                                                 const uint32_t *__restrict__ ptrack,
                                                                 const uint32_t *__restrict__ pt,
@@ -246,16 +236,12 @@ __global__ __launch_bounds__(kSortThreads, AID_K4_LDS3 ? 3 : 2) void k_radix_sca
                                                                 uint64_t *__restrict__ vals_out,
                                                                 uint32_t *__restrict__ E,
                                                                 uint16_t *__restrict__ sig_out) {
-#if AID_K4_LDS3
-    // the per-wave counters live in the front of the key staging area (52 KB per workgroup: three per CU): every
-    // posting's staging position is taken from them before the barrier that precedes the staging
+    // the per-wave counters (running counts, then cross-wave offsets) live in the front of the key staging area
+    // (52 KB per workgroup: three per CU): every posting's staging position is taken from them before the barrier that
+    // precedes the staging
     static_assert(kSortWaves * kDigits <= kTile, "counters fit the key staging area");
     __shared__ uint32_t s_key[kTile];
     uint32_t(*cnt)[kDigits] = reinterpret_cast<uint32_t(*)[kDigits]>(s_key);
-#else
-    __shared__ uint32_t s_key[kTile];
-    __shared__ uint32_t cnt[kSortWaves][kDigits];  // running per-wave counters, then cross-wave offsets
-#endif
     __shared__ uint64_t s_val[kTile];
     __shared__ uint32_t t_start[kDigits];          // first local position of each digit in the tile
     __shared__ uint32_t g_start[kDigits];          // global position of (digit, tile)
@@ -371,9 +357,7 @@ __global__ __launch_bounds__(kSortThreads, AID_K4_LDS3 ? 3 : 2) void k_radix_sca
         const uint32_t d = (key[s] >> shift) & (kDigits - 1);
         rank[s] = base + s * 64 + lane < n ? t_start[d] + cnt[w][d] + rank[s] : (uint32_t)kTile;
     }
-#if AID_K4_LDS3
     __syncthreads();
-#endif
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) {
         const uint32_t pos = rank[s];
@@ -389,15 +373,8 @@ __global__ __launch_bounds__(kSortThreads, AID_K4_LDS3 ? 3 : 2) void k_radix_sca
     for (int i = tid; i < m; i += kSortThreads) {
         const uint32_t k = s_key[i];
         const uint32_t d = (k >> shift) & (kDigits - 1);
-#if AID_K4_DIAG == 2
-        const int64_t dst = tile0 + i;  // timing-only: the sorted tile written back in place (sequential writes)
-#else
         const int64_t dst = (int64_t)g_start[d] + (i - (int)t_start[d]);
-#endif
         if (dst >= n) continue;  // cannot happen for consistent counts; never write out of bounds
-#if AID_K4_DIAG == 3
-        if (k != 0xFFFFFFFEu) continue;  // timing-only: no global writes (a key that never occurs)
-#endif
         if (LAST) {
             // the run ends of the CSR, from the sorted tile itself (no key array is written): inside a digit run
             // the tile's items are in full key order (stable passes), so a key change there is the key's last
