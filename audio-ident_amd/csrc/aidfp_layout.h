@@ -15,10 +15,7 @@ constexpr int kMaskWords = kBins / 64;  // 16 x u64 peak bitmask per frame
 
 // K1: kStftWaves waves per workgroup, one workgroup per CU: 16 waves (4 per SIMD at <= 128 VGPRs),
 // each with a private exchange buffer, + 24.5 KB of tables fit the 160 KB LDS
-#ifndef AID_K1_WAVES
-#define AID_K1_WAVES 16  // A/B builds only (engine.cpp and stft.hip alike)
-#endif
-constexpr int kStftWaves = AID_K1_WAVES;
+constexpr int kStftWaves = 16;
 constexpr int kStftStrip = 16;   // frames per wave at least, for large batches (one ring fill per range)
 constexpr int kK1MinFrames = 2;  // frames per wave at least, for small batches
 // float2 entries of a wave's exchange buffer: E1's 32 regions of 64 dwords at shifted bases (2108 dwords),

@@ -233,18 +233,11 @@ struct QueryParams {
 // A wave takes ceil(n / (waves x rounds)) <= 64 records at a time, rounds = ceil(n / (64 waves)),
 // so the records spread evenly over every wave (config 4's windows: ~650 records, which 64-record
 // groups had left on 11 of 16 waves).
-#ifndef AID_K5_CHUNK
-#define AID_K5_CHUNK 1  // A/B builds only: 0 = 64-record groups
-#endif
 template <int U, typename G>
 __device__ __forceinline__ void for_each_window(const QueryParams &qp, int64_t a, int64_t n, int wave, int nw, int lane,
                                                 G &&g) {
-#if AID_K5_CHUNK
     const int64_t rounds = (n + (int64_t)nw * 64 - 1) / ((int64_t)nw * 64);
     const int64_t chunk = rounds ? (n + nw * rounds - 1) / (nw * rounds) : 64;
-#else
-    const int64_t chunk = 64;
-#endif
     for (int64_t base = (int64_t)wave * chunk; base < n; base += (int64_t)nw * chunk) {
         const int64_t i = base + lane;
         uint32_t p0 = 0, len = 0;
@@ -548,32 +541,14 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 // 2-B signatures one per lane 3.64-3.74 (bytes were not the bound: the walk's ~95 instructions per 64 votes were)
 // -> 4-posting chunks 2.71-2.76 -> hot-vote queue 2.68 -> 8-posting chunks, four 512-thread workgroups per CU, the
 // LDS path up to 2^18 votes per query 1.80-1.86.
-#ifndef AID_K5_LDS8
-#define AID_K5_LDS8 1  // A/B builds only: 0 = 16-bit counters
-#endif
-#ifndef AID_K5_LDS_THREADS
-#define AID_K5_LDS_THREADS 512
-#endif
-#ifndef AID_K5_SIG_U
-#define AID_K5_SIG_U 3  // A/B builds only (more spill at the 64 VGPRs of 8 waves per SIMD)
-#endif
-constexpr int kLdsSigWindows = AID_K5_SIG_U;  // windows of 64 two-byte signature loads a wave keeps in flight
-#ifndef AID_K5_HBITS
-#define AID_K5_HBITS 15  // A/B builds only (with AID_K5_VCAP / AID_K5_TCAP / AID_K5_WPE)
-#endif
-constexpr int kLdsHistBits = AID_K5_HBITS;
-constexpr int kLdsCtrBits = AID_K5_LDS8 ? 8 : 16;
+constexpr int kLdsSigWindows = 3;  // windows of 64 two-byte signature loads a wave keeps in flight
+constexpr int kLdsHistBits = 15;
+constexpr int kLdsCtrBits = 8;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
-#ifndef AID_K5_VCAP
-#define AID_K5_VCAP (AID_K5_LDS8 ? 1024 : 4096)
-#endif
-constexpr int kFastVoteCap = AID_K5_VCAP;
-#ifndef AID_K5_TCAP
-#define AID_K5_TCAP 512
-#endif
-constexpr int kFastTrackCap = AID_K5_TCAP;
-constexpr int kFastThreads = AID_K5_LDS_THREADS;
+constexpr int kFastVoteCap = 1024;
+constexpr int kFastTrackCap = 512;
+constexpr int kFastThreads = 512;
 
 static_assert(kLdsHistBits <= 16, "the LDS filter's buckets come from 16-bit posting signatures");
 // kLdsMaxVotes (aidfp_layout.h): a heavier query reports nrows = -1 at once and the host runs it on the global path
@@ -586,10 +561,7 @@ static_assert(kLdsHistBits <= 16, "the LDS filter's buckets come from 16-bit pos
 // (record cursor, positions) is paid once per 64 C votes instead of once per 64: with one posting per lane the walk
 // issued ~63 VALU + 32 SALU per 64 votes and was the LDS path's cost (r05e: without its second enumeration K5 took
 // 1.76 of 3.63 ms, without the first pass's LDS atomics 3.24).
-#ifndef AID_K5_CW
-#define AID_K5_CW 8  // A/B builds only: postings per chunk, 4 (8-B loads) or 8 (16-B loads)
-#endif
-constexpr int kSigChunk = AID_K5_CW;
+constexpr int kSigChunk = 8;
 static_assert(kSigChunk == 4 || kSigChunk == 8, "signature chunks of 4 or 8 postings");
 typedef uint32_t sig_chunk_t __attribute__((ext_vector_type(kSigChunk / 2)));
 
@@ -719,9 +691,6 @@ __device__ __forceinline__ void sig_votes(const QueryParams &qp, int64_t a, int6
     else for_each_chunk<kLdsSigWindows>(qp, a, n, wave, nw, lane, g);
 }
 
-#ifndef AID_K5_HOTQ
-#define AID_K5_HOTQ 1  // A/B builds only: 0 = each hot vote's posting loaded inside the walk
-#endif
 // hot votes queued by the insert pass (posting index, tq): the LDS the counters leave beside the exact table
 constexpr int kTableBytes = kFastVoteCap * (8 + 3 * 4) + kFastTrackCap * (4 + 8);
 constexpr int kHotQueue = ((1 << kLdsHistBits) / kLdsCtrPerWord * 4 - kTableBytes) / 8;
@@ -744,14 +713,9 @@ static_assert(kHotQueue >= 256 && sizeof(FastLds::u) == (1 << kLdsHistBits) / kL
               "the hot-vote queue lives in the counters' LDS beside the exact table");
 
 __global__ __launch_bounds__(kFastThreads)
-#if AID_K5_LDS8
-#ifndef AID_K5_WPE
-#define AID_K5_WPE 8
-#endif
-__attribute__((amdgpu_waves_per_eu(AID_K5_WPE)))
-#endif
+__attribute__((amdgpu_waves_per_eu(8)))
 void k_match_lds(QueryParams qp) {
-    __shared__ FastLds L;  // 8-bit counters: 72 KB, two workgroups per CU (16-bit: 136 KB, one)
+    __shared__ FastLds L;  // 2^15 8-bit counters + the exact table / hot-vote queue: 36 KB, four workgroups per CU
     const int q = blockIdx.x;
     // a query heavier than the LDS filter suits goes to the global path at once, by its own vote count (a heavy
     // query here would wrap many 8-bit counters, mark their buckets hot and likely overflow the exact table after a
@@ -764,32 +728,20 @@ void k_match_lds(QueryParams qp) {
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t mm = (uint32_t)qp.min_match;
     for (int i = tid; i < (1 << kLdsHistBits) / kLdsCtrPerWord; i += kFastThreads) L.u.hist[i] = 0u;
-    if (AID_K5_LDS8)
-        for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
+    for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
     if (tid == 0) { L.out_n = 0; L.overflow = 0; L.hq_n = 0; }
     __syncthreads();
     // the query's exact vote total (k_query_votes): below the counter maximum no counter can wrap, so only
     // heavier queries pay for returning atomics (the carry check below)
     const bool check_wrap = qp.votes[q] >= (int64_t)kLdsCtrMax;
     // a query whose records fit one group per wave (<= 64 x waves: config 4's ~650) loads them once for both passes
-#ifndef AID_K5_REUSE
-#define AID_K5_REUSE 1  // A/B builds only
-#endif
     ChunkGroup grp_one{0u, 0u, 0u, 0u, 0u, 0};
-    const bool one_group = AID_K5_REUSE && n <= (int64_t)nw * 64;
+    const bool one_group = n <= (int64_t)nw * 64;
     if (one_group) {
         const int64_t chunk = group_records(n, nw);
         grp_one = load_group(qp, a, n, (int64_t)wave * chunk, chunk, lane);
     }
 
-#ifndef AID_K5_DIAG
-#define AID_K5_DIAG 0  // timing-only builds (wrong rows): 1 = phase 1 without its LDS atomics, 2 = no phase 3, 3 = both
-#endif
-#if AID_K5_DIAG & 1
-    uint32_t diag_x = 0;
-    sig_votes(qp, a, n, wave, nw, lane, one_group, grp_one, [&](uint32_t h) { diag_x += h; });
-    if (diag_x == 0xFFFFFFFFu) L.overflow = 2;  // keeps the loads
-#else
     // phase 1: every vote counted from its posting's 2-B signature alone (bucket = sig - tq = H(track) + d)
     sig_votes(qp, a, n, wave, nw, lane, one_group, grp_one, [&](uint32_t h) {
         const uint32_t sh = kLdsCtrBits * (h % kLdsCtrPerWord);
@@ -797,7 +749,6 @@ void k_match_lds(QueryParams qp) {
         if (check_wrap) {
             const uint32_t old = atomicAdd(w, 1u << sh);
             if (((old >> sh) & kLdsCtrMax) == kLdsCtrMax) {
-#if AID_K5_LDS8
                 // wrapped: the bucket holds >= 256 votes, so it is hot whatever its counter ends at;
                 // the carry went on into the next counters of the word, and through each full one
                 atomicOr(&L.hot[h >> 5], 1u << (h & 31));
@@ -805,17 +756,11 @@ void k_match_lds(QueryParams qp) {
                     const uint32_t hj = (h & ~3u) + j;
                     atomicOr(&L.hot[hj >> 5], 1u << (hj & 31));
                 }
-#else
-                // a 16-bit counter at 0xFFFF would carry into its neighbour: hand the query to
-                // the global path (exactness over speed)
-                L.overflow = 1;
-#endif
             }
         } else {
             atomicAdd(w, 1u << sh);
         }
     });
-#endif
     __syncthreads();
     if (L.overflow) {  // uniform: the global path answers this query
         if (tid == 0) qp.nrows[q] = -1;
@@ -831,8 +776,7 @@ void k_match_lds(QueryParams qp) {
             for (int b = 0; b < kLdsCtrPerWord; ++b)
                 bits |= (uint32_t)(((v >> (kLdsCtrBits * b)) & kLdsCtrMax) >= mm) << (kLdsCtrPerWord * j + b);
         }
-        if (AID_K5_LDS8) L.hot[w] |= bits;  // with the buckets phase 1 found wrapped
-        else L.hot[w] = bits;
+        L.hot[w] |= bits;  // with the buckets phase 1 found wrapped
     }
     __syncthreads();
     for (int i = tid; i < kFastVoteCap; i += kFastThreads) {
@@ -884,7 +828,7 @@ void k_match_lds(QueryParams qp) {
                 const int e = __builtin_ctz(hm[u]);
                 hm[u] &= hm[u] - 1;
                 const uint32_t pi = (uint32_t)kSigChunk * cid[u] + (uint32_t)e;
-                const int slot = AID_K5_HOTQ ? atomicAdd(&L.hq_n, 1) : kHotQueue;
+                const int slot = atomicAdd(&L.hq_n, 1);
                 if (slot < kHotQueue) {
                     L.u.t.hq[slot] = make_uint2(pi, (uint32_t)tqs[u]);
                 } else {  // queue full: this vote's posting now (a dependent load: one memory latency)
@@ -894,10 +838,8 @@ void k_match_lds(QueryParams qp) {
                 }
             }
     };
-    if (!(AID_K5_DIAG & 2)) {
-        if (one_group) walk_group<kLdsSigWindows>(grp_one, lane, insert_pass);
-        else for_each_chunk<kLdsSigWindows>(qp, a, n, wave, nw, lane, insert_pass);
-    }
+    if (one_group) walk_group<kLdsSigWindows>(grp_one, lane, insert_pass);
+    else for_each_chunk<kLdsSigWindows>(qp, a, n, wave, nw, lane, insert_pass);
     __syncthreads();
     // the queued hot votes: every thread loads its entries' postings at once (one memory latency for the whole
     // queue instead of one per hot vote inside the walk), then inserts them

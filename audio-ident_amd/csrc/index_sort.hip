@@ -45,15 +45,9 @@ constexpr int kSortKeyBits = 27;  // key26 plus the removed-posting sentinel 2^2
 constexpr int kDigitBits = 9;
 constexpr int kDigits = 1 << kDigitBits;
 constexpr int kSortPasses = 3;
-#ifndef AID_K4_THREADS
-#define AID_K4_THREADS 256  // A/B builds only
-#endif
-constexpr int kSortThreads = AID_K4_THREADS;  // 4 waves
+constexpr int kSortThreads = 256;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
-#ifndef AID_K4_SLOTS
-#define AID_K4_SLOTS 16  // A/B builds only (build_ext variant defines)
-#endif
-constexpr int kSlots = AID_K4_SLOTS;            // 64-item slots per wave
+constexpr int kSlots = 16;  // 64-item slots per wave
 constexpr int kTile = kSortThreads * kSlots;    // 4096 postings per tile
 constexpr int kDigitsPerThread = kDigits / kSortThreads;
 static_assert(kDigitBits * kSortPasses == kSortKeyBits, "passes cover the key");
@@ -134,10 +128,7 @@ __global__ __launch_bounds__(kSortThreads) void k_radix_count(const uint32_t *__
 }
 
 // ---- (digit, tile) starts from the tile-major counts: offs[t][d] = sum_{d' < d} total[d'] + sum_{t' < t} counts[t'][d]
-#ifndef AID_K4_COLTILES
-#define AID_K4_COLTILES 256  // A/B builds only
-#endif
-constexpr int kColTiles = AID_K4_COLTILES;  // tiles per column-sum group
+constexpr int kColTiles = 256;  // tiles per column-sum group
 __global__ __launch_bounds__(kDigits) void k_col_sum(const uint32_t *__restrict__ counts, int64_t tiles,
                                                      uint32_t *__restrict__ gsum) {
     const int d = threadIdx.x;

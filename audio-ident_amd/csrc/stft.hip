@@ -73,16 +73,8 @@ __device__ __forceinline__ uint64_t group16(uint64_t m) {
 }
 
 // power-row store, non-temporal (streaming): K1 0.268 -> 0.266 ms, K2 0.134 -> 0.130 ms same-box (r02)
-// (AID_K1_NTSTORE=0, A/B builds only: plain stores)
-#ifndef AID_K1_NTSTORE
-#define AID_K1_NTSTORE 1
-#endif
 __device__ __forceinline__ void pstore(float *p, float v) {
-#if AID_K1_NTSTORE
     __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
 }
 
 // E3 slot of Z[k] = 4 (k & 255) + (j2 ^ 2 h), j2 = k >> 8, h = bit 3 of k: the four Z[k + 256 j2] sit in one
@@ -92,20 +84,13 @@ __device__ __forceinline__ void pstore(float *p, float v) {
 // written by lane 3 of stage C.
 // PCM ring loads are non-temporal: K1 reads each sample once, and streaming it past the caches leaves the Infinity
 // Cache to the hot power rows K2 reads next (K2 -2 %, step -0.8 %, K1 unchanged in a 3-round same-box A/B,
-// profiles/r04q_k1_ntload_ab.txt). AID_K1_NTLOAD=0 (A/B builds only) restores plain loads
-#ifndef AID_K1_NTLOAD
-#define AID_K1_NTLOAD 1
-#endif
+// profiles/r04q_k1_ntload_ab.txt)
 // A clip may start at an odd sample (device clips, the exact lane's in-place sub-windows), so a frame's sample
 // pairs are only 4-byte aligned: they are read through a 2-float vector type declared 4-byte aligned (the same
 // global_load_dwordx2; a float2 pointer would promise the compiler 8 bytes)
 typedef float aid_f2u __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ float2 pcm_ld(const aid_f2u &r) {
-#if AID_K1_NTLOAD
     const aid_f2u v = __builtin_nontemporal_load(&r);
-#else
-    const aid_f2u v = r;
-#endif
     return make_float2(v.x, v.y);
 }
 #define AID_PCM(ref) pcm_ld(ref)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timing-only probe for the K1/K2 overlap (option (a) "K1/K2 fusion"): can K2 of one half of the
 batch run beside K1 of the other half? The default K1 takes 16 waves and 160,768 B of LDS per CU, so nothing runs
-beside it; a 12-wave K1 (AID_K1_WAVES=12 build: 125,824 B, 3 waves per SIMD at 122 VGPRs) leaves room for one K2
+beside it; a 12-wave K1 (the AID_K1_WAVES=12 build of commit 2556354; the knob was resolved to 16 afterwards:
+125,824 B, 3 waves per SIMD at 122 VGPRs) leaves room for one K2
 workgroup (21 KB, 124 VGPRs) per CU. The probe runs the bench's 256 x 10 s batch as
   single: one engine, one stream, 256 clips per step (the bench's step);
   dual:   two engines on two streams, 128 clips each, issued alternately, so engine B's K1 can overlap engine A's K2/K3;
