@@ -275,6 +275,10 @@ class FingerprintService:
         """Queue one query for the coalescer; returns a concurrent.futures.Future of list[OlafMatch]."""
         return self._coalescer.submit(pcm)
 
+    def submit_query_async(self, pcm: bytes):
+        """Queue one query from a running event loop; returns an asyncio future of list[OlafMatch]."""
+        return self._coalescer.submit_async(pcm)
+
     def query(self, pcm: bytes) -> list[OlafMatch]:
         return self._coalescer(pcm)
 
@@ -413,8 +417,9 @@ async def olaf_query(pcm_16k_f32le: bytes) -> list[OlafMatch]:
     if not pcm_16k_f32le:
         return []
     try:
-        # coalesced with the other queries in flight (one engine call per batch); no worker thread waits
-        return await asyncio.wrap_future(get_service().submit_query(pcm_16k_f32le))
+        # coalesced with the other queries in flight (one engine call per batch); no worker thread waits, and the
+        # batch's results reach this loop in one callback
+        return await get_service().submit_query_async(pcm_16k_f32le)
     except OlafError:
         raise
     except Exception as exc:

@@ -99,3 +99,54 @@ def test_coalescer_window_opens_only_under_load():
     assert [f.result(5) for f in futs] == list(range(8))
     assert seen[-1] == 8  # taken together
     c.close()
+
+
+def test_coalescer_async_requests_resolved_per_batch():
+    """submit_async (olaf_query's path): every coroutine gets its own result, in one thread-safe callback per loop
+    and batch rather than one per request; a failing batch fails its requests only; a request cancelled while its
+    batch runs is skipped."""
+    import asyncio
+
+    release = threading.Event()
+
+    def run(batch):
+        release.wait(5)
+        if any(p == "bad" for p in batch):
+            raise ValueError("bad batch")
+        return [p * 2 for p in batch]
+
+    c = QueryCoalescer(run, window_s=0.05)
+    calls = []
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        orig = loop.call_soon_threadsafe
+
+        def counting(cb, *a, **k):
+            calls.append(cb)
+            return orig(cb, *a, **k)
+
+        loop.call_soon_threadsafe = counting
+        first = c.submit_async(0)  # a lone first batch: dispatched at once
+        await asyncio.sleep(0.01)
+        futs = [c.submit_async(i) for i in range(1, 33)]  # queued while batch 1 waits: one batch of 32
+        release.set()
+        assert await first == 0
+        res = await asyncio.gather(*futs)
+        assert res == [2 * i for i in range(1, 33)]
+        n_before = len(calls)
+        bad = [c.submit_async("bad"), c.submit_async(5)]
+        out = await asyncio.gather(*bad, return_exceptions=True)
+        assert all(isinstance(x, ValueError) for x in out)
+        assert len(calls) - n_before <= 2
+        late = c.submit_async(7)
+        late.cancel()
+        assert await c.submit_async(8) == 16
+        return len(calls)
+
+    try:
+        n = asyncio.run(main())
+    finally:
+        c.close()
+    # batches: {0}, {1..32}, {bad, 5} (maybe split), {7, 8} (maybe split): far fewer callbacks than the 37 requests
+    assert n <= 8, n
