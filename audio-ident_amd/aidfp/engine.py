@@ -104,6 +104,38 @@ def _register_hook() -> None:
         _hook_registered = True
 
 
+_COPY_THREADS = 4
+_COPY_MIN = 1 << 22  # floats (16 MiB): smaller batches are copied by the calling thread alone. Same-box A/B on the
+#                      service leg (profiles/r05w5_service_copy_ab.jsonl): 64 clients (20 MB batches) 26.6-27.5 k qps
+#                      against 24.9-26.4 k single-threaded; from 4 MiB the 16-client batches (5 MB) lost 7-10 %
+_copy_pool = None
+_copy_pool_lock = threading.Lock()
+
+
+def _concat_into(arrs: list[np.ndarray], out: np.ndarray) -> None:
+    """np.concatenate(arrs, out=out), split over a few threads for large batches: a coalesced batch of 64 five-second
+    16 kHz queries is 20 MB, which one thread copies in ~2-4 ms -- most of a service batch's host time -- while
+    numpy releases the GIL inside each slice assignment."""
+    global _copy_pool
+    if len(out) < _COPY_MIN or len(arrs) < 2 * _COPY_THREADS:
+        np.concatenate(arrs, out=out)
+        return
+    if _copy_pool is None:
+        with _copy_pool_lock:
+            if _copy_pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                _copy_pool = ThreadPoolExecutor(_COPY_THREADS, thread_name_prefix="aidfp-pcm-copy")
+    ends = np.cumsum([len(a) for a in arrs])
+
+    def part(k: int) -> None:
+        for i in range(k, len(arrs), _COPY_THREADS):
+            out[ends[i] - len(arrs[i]): ends[i]] = arrs[i]
+
+    for f in [_copy_pool.submit(part, k) for k in range(_COPY_THREADS)]:
+        f.result()
+
+
 def _host_concat(arrs: list[np.ndarray], total: int) -> np.ndarray:
     """The clips concatenated into one host array for AID_PCM_HOST. Up to _PINNED_MAX samples it is a page-locked
     buffer of the calling thread (grown on demand), so the engine's single H2D copy of the span runs as a DMA
@@ -125,7 +157,7 @@ def _host_concat(arrs: list[np.ndarray], total: int) -> np.ndarray:
                     raise RuntimeError("interpreter shutting down")
                 buf = sl.buf = torch.empty(max(total, 1 << 20), dtype=torch.float32, pin_memory=True)
             out = buf.numpy()[:total]
-            np.concatenate(arrs, out=out)
+            _concat_into(arrs, out)
             return out
         except (ImportError, RuntimeError):  # no torch / no device: pageable memory works the same, slower
             pass

@@ -3,7 +3,7 @@
 # per-request wrap_future path of r05zz / r05zf; adapter and concurrency GPU tests first. Two service runs.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05w2
+O=gpurun_out/r05w3
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_adapter.py tests/test_gpu_concurrency.py tests/test_gpu_exact.py -x -q --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || exit 4
 for i in 1 2; do

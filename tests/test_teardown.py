@@ -65,3 +65,20 @@ def test_del_is_a_noop_after_shutdown():
         E._shutdown_done = saved
     eng.close()
     assert calls == [7]
+
+
+def test_host_concat_threaded_equals_concatenate(monkeypatch):
+    """The multi-threaded host batch copy (large coalesced batches) lays the clips out exactly as np.concatenate."""
+    import numpy as np
+
+    from aidfp import engine as E
+
+    rng = np.random.default_rng(3)
+    arrs = [rng.random(int(rng.integers(0, 50000))).astype(np.float32) for _ in range(37)]
+    out = np.empty(sum(len(a) for a in arrs), np.float32)
+    monkeypatch.setattr(E, "_COPY_MIN", 1)
+    E._concat_into(arrs, out)
+    assert np.array_equal(out, np.concatenate(arrs))
+    small = np.empty(10, np.float32)
+    E._concat_into([np.arange(4, dtype=np.float32), np.arange(6, dtype=np.float32)], small)
+    assert np.array_equal(small, np.concatenate([np.arange(4), np.arange(6)]).astype(np.float32))
