@@ -398,3 +398,33 @@ def test_csr_export_needs_a_finalized_index():
         assert len(posts) == len(rec)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("mode", ["sort", "ballot"])
+@pytest.mark.parametrize("n", [1, 100, 4096, 4097, 3 * 4096 + 5])
+def test_csr_layout_small_and_tile_edges(mode, n):
+    """K4 at the tile edges (a single posting, a partial tile, exactly one tile, one posting past it, several tiles
+    and a remainder), random hashes with many collisions and one removed track: the CSR equals the stable mirror."""
+    rng = np.random.default_rng(n)
+    h = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    h[rng.random(n) < 0.5] = np.uint32(0x12345678)  # half the postings in one bucket: long runs across tiles
+    tr = rng.integers(0, 7, n).astype(np.uint32)
+    t = rng.integers(0, 5000, n).astype(np.uint32)
+    eng = Engine(SR)
+    try:
+        eng.force("k4_build", {"sort": 1, "ballot": 4}[mode])
+        eng.index_add_postings(h.ctypes.data, tr.ctypes.data, t.ctypes.data, n, device=False)
+        removed = {3} if n > 1 else set()
+        for r in removed:
+            if (tr == r).any():
+                eng.index_remove(r)
+            else:
+                removed = set()
+        eng.index_finalize()
+        offs, posts = eng.index_csr()
+        post = eng.index_export()
+    finally:
+        eng.close()
+    ref_offs, ref_posts = _csr_mirror(post, removed)
+    assert np.array_equal(posts, ref_posts)
+    assert np.array_equal(offs, ref_offs)
