@@ -21,6 +21,7 @@ AID_PCM_HOST = 0
 AID_PCM_DEVICE = 1
 AID_FLAG_KEEP_POWER = 1
 AID_SYNTH_STATIONARY = 1
+AID_SYNTH_ASYNC = 2
 (AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD,
  AID_FORCE_EXCHANGE_FAIL, AID_FORCE_LANE_GATHER) = 1, 2, 3, 4, 5, 6, 7
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)

@@ -230,7 +230,9 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
         pcm = torch.empty(nb * n, dtype=torch.float32, device="cuda")
         src = torch.empty(nb * n_src, dtype=torch.float32, device="cuda") if resample else None
         # one non-default stream for generation, extraction and the posting append: events recorded on
-        # the legacy default stream would serialise against the engine's (blocking) stream every batch
+        # the legacy default stream would serialise against the engine's (blocking) stream every batch.
+        # Nothing in the loop waits for its own batch (the generation is enqueued, the append scans its
+        # counts on the device): the host runs ahead and the GPU goes from batch to batch without a gap
         s = torch.cuda.Stream()
         torch.cuda.synchronize()
         for b0 in range(0, len(mine), batch):
@@ -239,12 +241,12 @@ def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=Non
             a.record(s)
             if resample:  # each track decoded at its own rate, then K6 to the engine's (ffmpeg -ar per file)
                 eng.synth(src.data_ptr(), tr, np.zeros(len(tr), np.int64), n_src, stream=s.cuda_stream,
-                          sample_rate=int(source_sr))
+                          sample_rate=int(source_sr), wait=False)
                 for c in range(len(tr)):
                     eng.resample_range(src.data_ptr() + 4 * c * n_src, 0, n_src, 1, int(source_sr), eng.sample_rate,
                                        0, n, pcm.data_ptr() + 4 * c * n, stream=s.cuda_stream)
             else:
-                eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream)
+                eng.synth(pcm.data_ptr(), tr, np.zeros(len(tr), np.int64), n, stream=s.cuda_stream, wait=False)
             b.record(s)
             ev.append((a, b))
             eng.extract_device(pcm.data_ptr(), np.arange(len(tr) + 1, dtype=np.int64) * n, s.cuda_stream)

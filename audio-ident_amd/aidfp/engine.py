@@ -303,14 +303,17 @@ class Engine:
         return out[:F]
 
     def synth(self, dst_ptr: int, tracks, starts, n: int, noise_a: int = 0, salt: int = 0,
-              stream: int | None = None, fmax_hz: int = 8000, sample_rate: int = 0, envelope: bool = True) -> None:
+              stream: int | None = None, fmax_hz: int = 8000, sample_rate: int = 0, envelope: bool = True,
+              wait: bool = True) -> None:
         """aidfp.synth's PCM into device memory [n_clips][n] (partials in [100, fmax_hz) Hz), sampled at
-        `sample_rate` (0 = the engine's rate); envelope=False: the v0 stationary notes."""
+        `sample_rate` (0 = the engine's rate); envelope=False: the v0 stationary notes. wait=False returns once
+        the generation is enqueued on `stream` (AID_SYNTH_ASYNC): the caller orders its reads on that stream."""
         tr = np.ascontiguousarray(tracks, dtype=np.uint32)
         st = np.ascontiguousarray(starts, dtype=np.int64)
         check(self._lib.aid_synth_rate(self._h, ctypes.c_void_p(dst_ptr), _p(tr), _p(st), len(tr), int(n),
                                        int(sample_rate) or self.sample_rate, int(noise_a), int(salt) & 0xFFFFFFFF,
-                                       int(fmax_hz), 0 if envelope else L.AID_SYNTH_STATIONARY,
+                                       int(fmax_hz), (0 if envelope else L.AID_SYNTH_STATIONARY)
+                                       | (0 if wait else L.AID_SYNTH_ASYNC),
                                        ctypes.c_void_p(stream) if stream else None))
 
     # -- index + match (FPSPEC 7) --

@@ -62,6 +62,8 @@ void launch_compact(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *
 void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
                                 const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s);
+void launch_append_offsets(const int64_t *counts, int n_clips, int64_t base, int64_t *dst_off, int64_t *total,
+                           hipStream_t s);
 void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                         const uint32_t *offsets, int64_t *votes, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
@@ -163,10 +165,20 @@ struct aid_engine {
     DevBuf<int64_t> counts;
     DevBuf<uint32_t> synth_tracks;
     DevBuf<int64_t> synth_starts;
+    uint8_t *h_synth = nullptr;  // pinned staging of aid_synth_rate's tracks + starts (AID_SYNTH_ASYNC returns early)
+    size_t h_synth_cap = 0;
+    hipEvent_t synth_ev = nullptr;
+    bool synth_ev_live = false;
 
     // index (FPSPEC 7): all postings (SoA source of truth) + the CSR built from them
     DevBuf<uint32_t> p_hash, p_track, p_t;
-    int64_t n_post = 0;
+    int64_t n_post = 0;  // exact unless post_pend: then the last aid_index_add_extracted's count is in flight
+    // aid_index_add_extracted appends without waiting for its clips' counts: K_append scans them on the device and
+    // the new total comes back to pinned h_npost behind add_ev; settle_postings() makes n_post exact again
+    DevBuf<int64_t> d_npost;
+    int64_t *h_npost = nullptr;
+    hipEvent_t add_ev = nullptr;  // after the last append's staging copies (and, if post_pend, its count copy)
+    bool add_live = false, post_pend = false;
     std::vector<uint8_t> h_tomb;  // per track id: 1 = removed
     DevBuf<uint8_t> tomb;
     uint32_t n_tracks = 0;        // max track id + 1
@@ -496,6 +508,11 @@ void aid_engine_destroy(aid_engine *e) {
     e->chk.release();
     if (e->h_desc) (void)hipHostFree(e->h_desc);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_synth) (void)hipHostFree(e->h_synth);
+    if (e->h_npost) (void)hipHostFree(e->h_npost);
+    e->d_npost.release();
+    if (e->synth_ev) (void)hipEventDestroy(e->synth_ev);
+    if (e->add_ev) (void)hipEventDestroy(e->add_ev);
     if (e->desc_ev) (void)hipEventDestroy(e->desc_ev);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
     if (e->d_tab) (void)hipFree(e->d_tab);
@@ -849,7 +866,7 @@ int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int6
                    void *stream) {
     if (!e || !dst || !tracks || !starts || n_clips < 0 || n < 0 || noise_a < 0 || sample_rate <= 0)
         return fail(AID_ERR_INVALID, "aid_synth: bad argument");
-    if (flags & ~AID_SYNTH_STATIONARY) return fail(AID_ERR_INVALID, "aid_synth: unknown flags");
+    if (flags & ~(AID_SYNTH_STATIONARY | AID_SYNTH_ASYNC)) return fail(AID_ERR_INVALID, "aid_synth: unknown flags");
     if (sample_rate > 384000) return fail(AID_ERR_INVALID, "aid_synth: sample_rate above 384 kHz");
     if (fmax_hz <= 100 || 2 * (int64_t)fmax_hz > sample_rate)
         return fail(AID_ERR_INVALID, "aid_synth: fmax_hz must be in (100, sample_rate / 2]");
@@ -857,18 +874,39 @@ int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int6
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = pick_stream(e, stream);
-    if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    const bool async = (flags & AID_SYNTH_ASYNC) != 0;
+    // the engine's last work on another stream may still read dst; on the same stream it is ordered already
+    if (e->last_stream && (!async || e->last_stream != s)) HIP_TRY(hipStreamSynchronize(e->last_stream));
     HIP_TRY(e->synth_tracks.reserve(n_clips));
     HIP_TRY(e->synth_starts.reserve(n_clips));
-    HIP_TRY(hipMemcpyAsync(e->synth_tracks.p, tracks, n_clips * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(e->synth_starts.p, starts, n_clips * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    // tracks + starts go up from pinned staging (the caller's arrays may be gone when an async copy runs); the
+    // previous call's copies must have left it
+    const size_t tb = ((size_t)n_clips * sizeof(uint32_t) + 7) & ~(size_t)7, need = tb + (size_t)n_clips * sizeof(int64_t);
+    if (e->synth_ev_live) {
+        HIP_TRY(hipEventSynchronize(e->synth_ev));
+        e->synth_ev_live = false;
+    }
+    if (need > e->h_synth_cap) {
+        if (e->h_synth) HIP_TRY(hipHostFree(e->h_synth));
+        e->h_synth = nullptr;
+        e->h_synth_cap = 0;
+        HIP_TRY(hipHostMalloc((void **)&e->h_synth, need));
+        e->h_synth_cap = need;
+    }
+    std::memcpy(e->h_synth, tracks, (size_t)n_clips * sizeof(uint32_t));
+    std::memcpy(e->h_synth + tb, starts, (size_t)n_clips * sizeof(int64_t));
+    HIP_TRY(hipMemcpyAsync(e->synth_tracks.p, e->h_synth, n_clips * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->synth_starts.p, e->h_synth + tb, n_clips * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (!e->synth_ev) HIP_TRY(hipEventCreateWithFlags(&e->synth_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(e->synth_ev, s));
+    e->synth_ev_live = true;
     {
         ProfScope ps(e, AID_K_SYNTH, s);
         launch_synth(dst, e->synth_tracks.p, e->synth_starts.p, n_clips, n, sample_rate, noise_a, salt, fmax_hz,
                      !(flags & AID_SYNTH_STATIONARY), e->d_sin, s);
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(s));
+    if (!async) HIP_TRY(hipStreamSynchronize(s));
     return AID_OK;
 }
 
@@ -1212,11 +1250,23 @@ static int ensure_tracks(aid_engine *e, uint32_t max_track_plus1, hipStream_t s)
     return AID_OK;
 }
 
+// the posting count of the last aid_index_add_extracted, if still in flight, made exact (the append's own
+// kernels are ordered before the event; a reader of n_post or of the planes calls this first)
+static int settle_postings(aid_engine *e) {
+    if (!e->add_live) return AID_OK;
+    HIP_TRY(hipEventSynchronize(e->add_ev));
+    e->add_live = false;
+    if (e->post_pend) e->n_post = *e->h_npost;
+    e->post_pend = false;
+    return AID_OK;
+}
+
 extern "C" {
 
 int aid_index_reset(aid_engine *e) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = settle_postings(e)) return rc;
     e->n_post = 0;
     e->n_tracks = 0;
     e->h_tomb.clear();
@@ -1234,8 +1284,10 @@ int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids) {
     hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
     const int n = e->n_clips;
     if (n == 0) return AID_OK;
-    // pinned staging [counts n][src n][dst n][tracks n/2+1] (int64 slots): the H2D copies below run
-    // asynchronously; the next call's counts sync orders its rewrite of the staging after them
+    // the previous call's count (normally long arrived: this batch's extraction was queued behind it) and its
+    // pinned staging, whose H2D copies precede that call's event
+    if (int rc = settle_postings(e)) return rc;
+    // pinned staging [counts n][src n][dst n][tracks n/2+1] (int64 slots)
     const size_t need = 3 * (size_t)n + (size_t)n / 2 + 1;
     if (need > e->h_stage_cap) {
         if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
@@ -1246,29 +1298,58 @@ int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids) {
     }
     int64_t *counts = e->h_stage, *src = counts + n, *dst = src + n;
     uint32_t *trk = reinterpret_cast<uint32_t *>(dst + n);
-    HIP_TRY(hipMemcpyAsync(counts, e->counts.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    int64_t tot = 0;
     uint32_t mx = 0;
     for (int c = 0; c < n; ++c) {
         src[c] = e->clip_base[c];
-        dst[c] = e->n_post + tot;
         trk[c] = track_ids[c];
-        tot += counts[c];
         mx = std::max(mx, track_ids[c] + 1);
     }
-    if (int rc = reserve_postings(e, tot, s)) return rc;
     if (int rc = ensure_tracks(e, mx, s)) return rc;
     HIP_TRY(e->x_src.reserve(n));
     HIP_TRY(e->x_dst.reserve(n));
     HIP_TRY(e->x_tracks.reserve(n));
-    HIP_TRY(hipMemcpyAsync(e->x_src.p, src, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(e->x_dst.p, dst, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(e->x_tracks.p, trk, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-    launch_records_to_postings(e->records.p, e->x_src.p, e->counts.p, e->x_dst.p, e->x_tracks.p, n, e->p_hash.p,
-                               e->p_track.p, e->p_t.p, s);
-    HIP_TRY(hipGetLastError());  // no sync: every reader of the posting planes syncs last_stream first
-    e->n_post += tot;
+    // the batch's postings are at most its hash capacity: when the planes hold that much more, the append is
+    // scanned on the device and nothing waits for it; otherwise the counts come back first and the planes grow
+    // to the exact need plus one batch's hash capacity (1.5x the records buffer the extraction already holds),
+    // so the following appends of such batches are asynchronous again (growth doubles: this path runs
+    // O(log n) times), unless that headroom would take more than a quarter of the free device memory
+    const int64_t bound = e->total_records;
+    const int64_t cap = (int64_t)std::min({e->p_hash.n, e->p_track.n, e->p_t.n});
+    if (!e->add_ev) HIP_TRY(hipEventCreateWithFlags(&e->add_ev, hipEventDisableTiming));
+    if (e->n_post + bound <= cap) {
+        if (!e->h_npost) HIP_TRY(hipHostMalloc((void **)&e->h_npost, sizeof(int64_t)));
+        HIP_TRY(e->d_npost.reserve(1));
+        HIP_TRY(hipMemcpyAsync(e->x_src.p, src, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->x_tracks.p, trk, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        launch_append_offsets(e->counts.p, n, e->n_post, e->x_dst.p, e->d_npost.p, s);
+        launch_records_to_postings(e->records.p, e->x_src.p, e->counts.p, e->x_dst.p, e->x_tracks.p, n, e->p_hash.p,
+                                   e->p_track.p, e->p_t.p, s);
+        HIP_TRY(hipMemcpyAsync(e->h_npost, e->d_npost.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(e->add_ev, s));
+        HIP_TRY(hipGetLastError());
+        e->add_live = e->post_pend = true;
+    } else {
+        HIP_TRY(hipMemcpyAsync(counts, e->counts.p, n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        int64_t tot = 0;
+        for (int c = 0; c < n; ++c) {
+            dst[c] = e->n_post + tot;
+            tot += counts[c];
+        }
+        size_t free_b = 0, total_b = 0;
+        HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+        const bool room = (size_t)bound * 3 * sizeof(uint32_t) <= free_b / 4;
+        if (int rc = reserve_postings(e, tot + (room ? bound : 0), s)) return rc;
+        HIP_TRY(hipMemcpyAsync(e->x_src.p, src, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->x_dst.p, dst, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->x_tracks.p, trk, n * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        launch_records_to_postings(e->records.p, e->x_src.p, e->counts.p, e->x_dst.p, e->x_tracks.p, n, e->p_hash.p,
+                                   e->p_track.p, e->p_t.p, s);
+        HIP_TRY(hipEventRecord(e->add_ev, s));  // the staging's copies (the next call waits for them)
+        HIP_TRY(hipGetLastError());  // no sync: every reader of the posting planes syncs last_stream first
+        e->add_live = true;
+        e->n_post += tot;
+    }
     e->index_dirty = true;
     return AID_OK;
 }
@@ -1281,6 +1362,7 @@ int aid_index_add_postings(aid_engine *e, const uint32_t *hash, const uint32_t *
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->own_stream;
+    if (int rc = settle_postings(e)) return rc;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     uint32_t mx = 0;
     if (location == AID_PCM_HOST) {
@@ -1329,6 +1411,7 @@ int aid_index_remove(aid_engine *e, uint32_t track) {
 int aid_index_compact(aid_engine *e, int64_t *n_removed) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
     std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = settle_postings(e)) return rc;
     if (n_removed) *n_removed = 0;
     bool any = false;
     for (uint8_t t : e->h_tomb) any = any || t;
@@ -1370,6 +1453,7 @@ int aid_index_compact(aid_engine *e, int64_t *n_removed) {
 
 static int finalize_locked(aid_engine *e) {
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc = settle_postings(e)) return rc;
     hipStream_t s = e->own_stream;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     if (e->n_post > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index holds more than 2^32 postings");
@@ -1461,6 +1545,8 @@ int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset) {
 
 int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks) {
     if (!e) return fail(AID_ERR_INVALID, "null engine");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = settle_postings(e)) return rc;
     if (n_postings) *n_postings = e->n_post;
     if (n_live) *n_live = e->index_built && !e->index_dirty ? e->n_indexed : -1;
     if (n_tracks) *n_tracks = e->n_tracks;
@@ -1534,6 +1620,7 @@ int aid_comm_size(const aid_comm *c, int32_t *world, int32_t *rank) {
 // the exchange in three steps (aid_index_allgather runs them around two RCCL all-gathers; a host-driven
 // exchange, e.g. torch.distributed over gloo, runs them around its own collectives)
 static int shard_info_locked(aid_engine *e, int64_t first, int64_t *count, uint32_t *n_tracks) {
+    if (int rc = settle_postings(e)) return rc;
     if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "index exchange: first out of range");
     *count = e->n_post - first;
     *n_tracks = e->n_tracks;
@@ -1545,6 +1632,7 @@ static int pack_locked(aid_engine *e, int64_t first, uint32_t *planes, int64_t s
         e->inject_exchange_fail = 0;
         return fail(AID_ERR_NOMEM, "index exchange: injected failure of this rank's pack (aid_engine_force)");
     }
+    if (int rc = settle_postings(e)) return rc;
     const int64_t n = e->n_post - first;
     if (n > stride) return fail(AID_ERR_INVALID, "aid_index_pack: stride below the shard's count");
     const uint32_t *src[3] = {e->p_hash.p, e->p_track.p, e->p_t.p};
@@ -1560,6 +1648,7 @@ static int pack_locked(aid_engine *e, int64_t first, uint32_t *planes, int64_t s
 // the posting planes and the tombstone buffer grow keeping every stored posting (n_post, not first) and
 // every tombstone; the index itself (n_post, n_tracks, the CSR) does not change
 static int splice_reserve_locked(aid_engine *e, int64_t first, int64_t tot, uint32_t n_tracks, hipStream_t s) {
+    if (int rc = settle_postings(e)) return rc;
     if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "index exchange: first out of range");
     if (tot < 0) return fail(AID_ERR_INVALID, "index exchange: negative posting count");
     if (first + tot > 0xFFFFFFFFll) return fail(AID_ERR_INVALID, "index exchange: more than 2^32 postings");
@@ -1574,6 +1663,7 @@ static int splice_reserve_locked(aid_engine *e, int64_t first, int64_t tot, uint
 // the index changes; the union then replaces [first, n_post) in one stream-ordered pass
 static int splice_locked(aid_engine *e, int64_t first, const uint32_t *recv, int32_t world, int64_t stride,
                          const int64_t *counts, uint32_t n_tracks, hipStream_t s) {
+    if (int rc = settle_postings(e)) return rc;
     if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "aid_index_splice: first out of range");
     int64_t tot = 0;
     for (int r = 0; r < world; ++r) {
@@ -1615,6 +1705,7 @@ int aid_index_reserve(aid_engine *e, int64_t first, int64_t total, uint32_t n_tr
 int aid_index_pack(aid_engine *e, int64_t first, uint32_t *planes, int64_t stride, void *stream) {
     if (!e || (!planes && stride > 0) || stride < 0) return fail(AID_ERR_INVALID, "aid_index_pack: bad argument");
     std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = settle_postings(e)) return rc;
     if (first < 0 || first > e->n_post) return fail(AID_ERR_INVALID, "aid_index_pack: first out of range");
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = pick_stream(e, stream);
@@ -1654,6 +1745,7 @@ int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_to
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->own_stream;
+    if (int rc = settle_postings(e)) return rc;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     const int W = c->world;
     // aid_comm_create reserved this engine's meta buffer; a comm made with another engine gets it here (16 B per
@@ -1731,9 +1823,11 @@ int aid_index_allgather(aid_engine *e, aid_comm *c, int64_t first, int64_t *n_to
 
 int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t, int64_t first, int64_t count,
                      int32_t location) {
-    if (!e || first < 0 || count < 0 || first + count > e->n_post) return fail(AID_ERR_INVALID, "aid_index_export: bad range");
-    if (count == 0) return AID_OK;
+    if (!e || first < 0 || count < 0) return fail(AID_ERR_INVALID, "aid_index_export: bad range");
     std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = settle_postings(e)) return rc;
+    if (first + count > e->n_post) return fail(AID_ERR_INVALID, "aid_index_export: bad range");
+    if (count == 0) return AID_OK;
     HIP_TRY(hipSetDevice(e->device));
     // the posting append of aid_index_add_extracted runs asynchronously on the caller's stream
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
@@ -1745,9 +1839,10 @@ int aid_index_export(aid_engine *e, uint32_t *hash, uint32_t *track, uint32_t *t
 }
 
 int aid_index_checksum(aid_engine *e, int64_t first, int64_t count, uint64_t *out) {
-    if (!e || !out || first < 0 || count < 0 || first + count > e->n_post)
-        return fail(AID_ERR_INVALID, "aid_index_checksum: bad range");
+    if (!e || !out || first < 0 || count < 0) return fail(AID_ERR_INVALID, "aid_index_checksum: bad range");
     std::lock_guard<std::mutex> lk(e->mu);
+    if (int rc = settle_postings(e)) return rc;
+    if (first + count > e->n_post) return fail(AID_ERR_INVALID, "aid_index_checksum: bad range");
     HIP_TRY(hipSetDevice(e->device));
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     HIP_TRY(e->chk.reserve(1));
@@ -1789,6 +1884,7 @@ int aid_index_save(aid_engine *e, const char *path) {
     if (!e || !path) return fail(AID_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc = settle_postings(e)) return rc;
     if (e->last_stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     FILE *f = std::fopen(path, "wb");
     if (!f) return fail(AID_ERR_INVALID, std::string("cannot open ") + path);
@@ -1812,6 +1908,7 @@ int aid_index_load(aid_engine *e, const char *path) {
     if (!e || !path) return fail(AID_ERR_INVALID, "null argument");
     std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
+    if (int rc = settle_postings(e)) return rc;
     // Everything is validated and read into scratch buffers first; the engine's index changes only
     // once the whole file has been read (a failed load leaves the previous index untouched).
     struct File {

@@ -186,6 +186,46 @@ __global__ void k_records_to_postings(const uint64_t *__restrict__ recs, const i
     }
 }
 
+// clips' posting counts -> their append offsets base + exclusive prefix, and the new posting total, in one
+// workgroup (a batch is at most a few thousand clips): the append needs no host round trip for the counts
+__global__ __launch_bounds__(1024) void k_append_offsets(const int64_t *__restrict__ counts, int n_clips, int64_t base,
+                                                         int64_t *__restrict__ dst_off, int64_t *__restrict__ total) {
+    __shared__ int64_t s_w[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int64_t run = base;
+    for (int c0 = 0; c0 < n_clips; c0 += 1024) {
+        const int c = c0 + tid;
+        const int64_t v = c < n_clips ? counts[c] : 0;
+        int64_t x = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) s_w[w] = x;
+        __syncthreads();
+        int64_t t = 0;  // wave 0: inclusive scan of the 16 wave sums
+        if (w == 0) {
+            t = lane < 16 ? s_w[lane] : 0;
+            for (int d = 1; d < 16; d <<= 1) {
+                const int64_t y = __shfl_up(t, d);
+                if (lane >= d) t += y;
+            }
+        }
+        __syncthreads();
+        if (w == 0 && lane < 16) s_w[lane] = t;
+        __syncthreads();
+        if (c < n_clips) dst_off[c] = run + (w ? s_w[w - 1] : 0) + x - v;
+        run += s_w[15];
+        __syncthreads();
+    }
+    if (tid == 0) *total = run;
+}
+
+void launch_append_offsets(const int64_t *counts, int n_clips, int64_t base, int64_t *dst_off, int64_t *total,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_append_offsets, dim3(1), dim3(1024), 0, s, counts, n_clips, base, dst_off, total);
+}
+
 void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, const int64_t *counts,
                                 const int64_t *dst_off, const uint32_t *track_ids, int n_clips, uint32_t *ph,
                                 uint32_t *ptrack, uint32_t *pt, hipStream_t s) {

@@ -158,6 +158,9 @@ int aid_synth_band(aid_engine *e, float *dst, const uint32_t *tracks, const int6
    flags: AID_SYNTH_STATIONARY = the v0 generator (constant amplitude within a note); default = v2 (every
    note decays linearly to half amplitude, as a struck or plucked note: landmark times lock to the onsets). */
 #define AID_SYNTH_STATIONARY 1
+/* flags: AID_SYNTH_ASYNC = return once the generation is enqueued on `stream` (ordered after the engine's
+   earlier work on that stream; the caller orders its own reads of dst). Default: the call waits for it. */
+#define AID_SYNTH_ASYNC 2
 int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int64_t *starts, int32_t n_clips,
                    int64_t n, int32_t sample_rate, int32_t noise_a, uint32_t salt, int32_t fmax_hz, int32_t flags,
                    void *stream);
@@ -178,7 +181,9 @@ typedef struct aid_match_row {
 } aid_match_row;
 
 int aid_index_reset(aid_engine *e);
-/* Add every clip of the last aid_extract as track track_ids[c] (host array of n_clips). */
+/* Add every clip of the last aid_extract as track track_ids[c] (host array of n_clips). Asynchronous: the
+   clips' posting counts are scanned on the device and the call does not wait for them (only for the previous
+   call's); every reader of the postings (stats, finalize, export, ...) waits for the count first. */
 int aid_index_add_extracted(aid_engine *e, const uint32_t *track_ids);
 /* Add n postings (hash, track, t) from host (AID_PCM_HOST) or device (AID_PCM_DEVICE) arrays. */
 int aid_index_add_postings(aid_engine *e, const uint32_t *hash, const uint32_t *track, const uint32_t *t, int64_t n,

@@ -428,3 +428,52 @@ def test_csr_layout_small_and_tile_edges(mode, n):
     ref_offs, ref_posts = _csr_mirror(post, removed)
     assert np.array_equal(posts, ref_posts)
     assert np.array_equal(offs, ref_offs)
+
+
+def test_async_append_equals_per_clip_records(tmp_path):
+    """aid_index_add_extracted appends without waiting for its batch's counts (offsets scanned on the device, the
+    new total read back by the next reader; engine.cpp settle_postings): batches of every size, a silent clip and
+    one shorter than a frame, readers and a host append between them, and batches beyond the planes' headroom
+    (the growth path, counts read back first) store exactly each clip's records under its track, in call order."""
+    sr = 16000
+    rng = np.random.default_rng(3)
+    with Engine(sr) as eng:
+        want, tid = [], 100
+
+        def rows(t, r):
+            return np.stack([(r & np.uint64(0xFFFFFFFF)).astype(np.uint32), np.full(len(r), t, np.uint32),
+                             (r >> np.uint64(32)).astype(np.uint32)], axis=1)
+
+        for b, k in enumerate([1, 4, 2, 7, 1, 3, 24, 2, 1]):
+            clips = [synth.synth(tid + j, int(rng.integers(0, 5 * sr)), int(rng.integers(2 * sr, 9 * sr)), sr,
+                                 snr_db=30.0, salt=b) for j in range(k)]
+            if b == 2:
+                clips += [np.zeros(3 * sr, np.float32), np.zeros(100, np.float32)]
+            recs = eng.extract_host(clips)
+            tracks = np.arange(tid, tid + len(clips), dtype=np.uint32)
+            eng.index_add_extracted(tracks)
+            want += [rows(t, r) for t, r in zip(tracks, recs)]
+            tid += len(clips)
+            if b == 3:
+                assert eng.index_stats()["postings"] == sum(map(len, want))
+            if b == 4:
+                eng.index_add_records(tid, recs[0])
+                want.append(rows(tid, recs[0]))
+                tid += 1
+            if b == 5:
+                assert np.array_equal(eng.index_export(), np.concatenate(want))
+            if b == 7:
+                path = tmp_path / "mid.aidfp"
+                eng.index_save(str(path))
+                with Engine(sr) as e2:
+                    e2.index_load(str(path))
+                    assert np.array_equal(e2.index_export(), np.concatenate(want))
+        post = eng.index_export()
+        assert np.array_equal(post, np.concatenate(want))
+        eng.index_finalize()
+        assert eng.index_stats()["live"] == len(post)
+        eng.index_reset()
+        assert eng.index_stats()["postings"] == 0
+        recs = eng.extract_host([synth.synth(7, 0, 4 * sr, sr), synth.synth(8, 0, 5 * sr, sr)])
+        eng.index_add_extracted(np.array([7, 8], np.uint32))
+        assert np.array_equal(eng.index_export(), np.concatenate([rows(7, recs[0]), rows(8, recs[1])]))
