@@ -245,7 +245,6 @@ struct aid_engine {
     int k5_parts = 0;      // aid_engine_force K5_PARTS: K5a key partitions per query (0 = by vote count)
     int lane_gather = 0;           // aid_engine_force LANE_GATHER: stage the exact lane's sub-windows (A/B)
     int inject_exchange_fail = 0;  // aid_engine_force EXCHANGE_FAIL: the next exchange's prepare step fails (tests)
-    bool k5_spec_ok = true;  // the previous query batch's heaviest query fitted the LDS path (speculation gate)
     // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
     int64_t st_queries = 0, st_votes = 0, st_post_reads = 0, st_q_global = 0, st_q_lds = 0, st_records = 0;
     int64_t st_sig_reads = 0;  // 2-B posting signatures the LDS path read (two per vote: counting and insert passes)
@@ -1982,7 +1981,6 @@ constexpr double kForwardedPerBucket = 2.0;  // forwarded votes (1-bit filter es
 // queries whose exact LDS table overflowed are re-run with 4x the buckets. (max_recs is unused.)
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
-constexpr int kSpeculateQueries = 16;  // run_queries: LDS match path launched with the vote counts
 
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
                        int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
@@ -2000,13 +1998,13 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(h_votes.data(), e->q_votes.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     }
-    // a few queries (a stream window, one upload's sub-windows): run the LDS path right away in the same
-    // round trip as the vote counts instead of after them (one host sync less per call). It is exact at
-    // any load (an overflowing query reports -1 and falls through to the global path below); only its
-    // speed suffers for heavy queries, which a handful of them bounds
-    // (gated on the previous batch: a heavy small batch, e.g. stream windows against a large catalog, would
-    // otherwise pay the slow LDS run before falling back every time)
-    const bool speculate = e->k5_path == 0 && nq <= kSpeculateQueries && e->k5_spec_ok;
+    // the LDS path is launched right away, in the same round trip as the vote counts instead of after them (one
+    // host sync less per call). It routes each query by its own count (K5 reads q_votes on the device): a query
+    // above kLdsMaxVotes is handed back (nrows -1) without an LDS run, and one that overflows its counters reports
+    // -1 too; both fall through to the global path below. Round 2 did this for batches of <= 16 queries, gated on
+    // the previous batch's heaviest query, because the LDS kernel then ran heavy queries too; with per-query
+    // routing (round 5) a batch of any size takes it, the coalesced service batches and the stream pushes included
+    const bool speculate = e->k5_path == 0;
     std::vector<int32_t> spec_n;
     if (speculate) {
         {
@@ -2034,7 +2032,6 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     int64_t vmax = 1;
     for (int q = 0; q < nq; ++q) vmax = std::max(vmax, h_votes[q]);
     const double votes = (double)vmax;
-    e->k5_spec_ok = 2.0 * votes <= 65536.0;
     e->st_queries += nq;
     for (int q = 0; q < nq; ++q) {
         e->st_votes += h_votes[q];
