@@ -198,7 +198,7 @@ def native_comm(eng, group=None) -> int:
     return eng.comm_create(obj[0], dist.get_world_size(group), rank)
 
 
-def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 512, group=None,
+def ingest_synthetic(eng, track_ids, seconds: float, batch: int = 256, group=None,
                      exchange: str = "native", source_sr: int | None = None, local: bool = False) -> IngestStats:
     """Fingerprint this rank's shard of synthetic tracks on its GPU, replicate the index.
 

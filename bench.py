@@ -421,7 +421,9 @@ def catalog_leg(args, rank, world, dist, torch) -> dict:
         t0 = time.perf_counter()
         # ingest agrees on its own rank-local steps (extraction, the exchange's prepare round); the last
         # agreement covers the index build
-        st = _agreed(lambda: ingest_synthetic(eng, tracks, args.catalog_seconds, batch=1024, exchange=exchange),
+        # 256 tracks per extraction call: K1/K2 run 5-14 % faster per audio-second on 2.7 GB power planes than on
+        # 1,024 tracks' 10.8 GB (profiles/r05zo_catalog_batch.txt)
+        st = _agreed(lambda: ingest_synthetic(eng, tracks, args.catalog_seconds, batch=256, exchange=exchange),
                      "catalog ingest", dist)
         torch.cuda.synchronize()
         if dist:

@@ -30,7 +30,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tracks", type=int, default=100000)
     ap.add_argument("--seconds", type=float, default=30.0)
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--sr", type=int, default=44100)
     ap.add_argument("--check", type=int, default=64, help="spot-check queries on rank 0")
     ap.add_argument("--exchange", choices=("native", "torch"), default="native",

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--wait-synth", action="store_true")
     ap.add_argument("--sr", type=int, default=16000)
+    ap.add_argument("--batch", type=int, default=1024, help="tracks per extraction call")
     ap.add_argument("--profile", action="store_true", help="one more pass with the engine's per-kernel events")
     args = ap.parse_args()
     import torch
@@ -36,7 +37,7 @@ def main():
     torch.cuda.set_device(0)
     eng = Engine(args.sr, device=0)
     n = int(round(args.seconds * args.sr)) & ~1
-    batch = 1024
+    batch = args.batch
     pcm = torch.empty(batch * n, dtype=torch.float32, device="cuda")
     s = torch.cuda.Stream()
     tracks = np.arange(args.tracks, dtype=np.uint32)
@@ -72,7 +73,7 @@ def main():
             print(json.dumps({"sr": args.sr, "wall_s": round(wall, 4), "kernel_ms_total": k}), flush=True)
             continue
         print(json.dumps({"lib": "AIDFP_LIB" in __import__("os").environ and "base" or "tree", "sr": args.sr,
-                          "wait_synth": args.wait_synth, "rep": rep, "wall_s": round(wall, 4),
+                          "wait_synth": args.wait_synth, "batch": batch, "rep": rep, "wall_s": round(wall, 4),
                           "synth_s": round(t_synth, 4), "ingest_s": round(wall - t_synth, 4),
                           "audio_s_per_s": round(args.tracks * args.seconds / (wall - t_synth), 1),
                           "postings": post, "checksum": hex(eng.index_checksum())}), flush=True)
