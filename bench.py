@@ -480,7 +480,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     """BASELINE config 4 against the catalog this leg just built (every rank holds the whole union): per rank
     args.exact_clips 5 s query clips of catalog tracks plus 10 % more from unseen tracks, at SNR 20 dB mixed at
     half gain as the reference corpus's noisy variant (bench_match.py "noise20"), through aid_exact_lane in
-    4096-clip calls (sub-window fan-out, K1-K5 and the consensus in one call; reference
+    args.exact_batch-clip calls (sub-window fan-out, K1-K5 and the consensus in one call; reference
     app/search/exact.py:70-353). value = all ranks' clips / the slowest rank's GPU time (weak scaling: queries
     are independent). Accuracy in the shape of scripts/eval_exact.py:46-54 (top-1 target 0.98 on clean). An
     untimed second pass of the same clips with events on the K5 kernels gives the match roofline: 8 B per
@@ -498,7 +498,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     starts = np.concatenate([rng.integers(0, int((args.catalog_seconds - 5.0) * SR), n_pos),
                              np.zeros(n_neg, np.int64)]).astype(np.int64)
     clip_n = 5 * SR
-    batch = 4096
+    batch = args.exact_batch
     a = types.SimpleNamespace(batch=batch, sr=SR)
     cat = CATEGORIES["noise20"]
 
@@ -511,7 +511,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
 
     def local():
         pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
-        w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a 4096-clip call is sized here
+        w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a full call is sized here
         run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
         res, t_gpu = run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, True, keep=sel)
         kept = res.pop("kept", {})
@@ -556,7 +556,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     return {"value": round(world * n / t_max, 1), "unit": "clips/s", "clips_per_rank": n, "positives_per_rank": n_pos,
             "negatives_per_rank": n_neg, "gpu_s_max_over_ranks": round(t_max, 4),
             "category": "noise20 (SNR 20 dB, gain 0.5)", "rank0": res, "match_stats": ms, "roofline": roof,
-            "parity": par, "path": "aid_exact_lane, 4096 clips per call, 3 sub-windows each"}
+            "parity": par, "path": f"aid_exact_lane, {batch} clips per call, 3 sub-windows each"}
 
 
 def _postings_where(eng, values: np.ndarray, torch, column: int = 0, chunk: int = 1 << 26) -> np.ndarray:
@@ -1015,6 +1015,7 @@ def main() -> int:
                          "printed without them and the process ends (0 = no deadline)")
     ap.add_argument("--catalog-tracks", type=int, default=100000)
     ap.add_argument("--catalog-seconds", type=float, default=30.0)
+    ap.add_argument("--exact-batch", type=int, default=4096, help="config-4 clips per aid_exact_lane call")
     ap.add_argument("--exact-clips", type=int, default=10000,
                     help="config-4 positive query clips per rank against the catalog leg's index, plus 10 %% "
                          "negatives from unseen tracks (BASELINE configs[3]: 10k; 0 = skip)")
