@@ -23,7 +23,7 @@ AID_FLAG_KEEP_POWER = 1
 AID_SYNTH_STATIONARY = 1
 AID_SYNTH_ASYNC = 2
 (AID_FORCE_K5_PATH, AID_FORCE_K5_PARTS, AID_FORCE_K5_BATCH, AID_FORCE_K2_STRIPS_X100, AID_FORCE_K4_BUILD,
- AID_FORCE_EXCHANGE_FAIL, AID_FORCE_LANE_GATHER) = 1, 2, 3, 4, 5, 6, 7
+ AID_FORCE_EXCHANGE_FAIL, AID_FORCE_LANE_GATHER, AID_FORCE_PLANE_ROWS) = 1, 2, 3, 4, 5, 6, 7, 8
 AID_K_STFT, AID_K_PEAKS, AID_K_LANDMARK_COUNT, AID_K_LANDMARK_WRITE, AID_K_SYNTH, AID_K_MATCH = range(6)
 AID_K_COUNT = 12
 KERNEL_NAMES = ["stft_power", "peak_pick", "landmark_count", "landmark_write", "synth", "match", "resample",

@@ -222,7 +222,8 @@ class Engine:
 
     FORCE = {"k5_path": L.AID_FORCE_K5_PATH, "k5_parts": L.AID_FORCE_K5_PARTS, "k5_batch": L.AID_FORCE_K5_BATCH,
              "k2_strips_x100": L.AID_FORCE_K2_STRIPS_X100, "k4_build": L.AID_FORCE_K4_BUILD,
-             "exchange_fail": L.AID_FORCE_EXCHANGE_FAIL, "lane_gather": L.AID_FORCE_LANE_GATHER}
+             "exchange_fail": L.AID_FORCE_EXCHANGE_FAIL, "lane_gather": L.AID_FORCE_LANE_GATHER,
+             "plane_rows": L.AID_FORCE_PLANE_ROWS}
 
     def force(self, what: str, value: int) -> None:
         """Test hook (aid_engine_force): pin one of the engine's own code paths, e.g. force("k5_path", 2)."""

@@ -22,12 +22,12 @@
 #include "resample_design.h"
 
 namespace aid {
-void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
+void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t f0, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
                        uint64_t *hot, float thr, bool keep_power, hipStream_t s);
 int peak_pick_blocks_per_cu();
-void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len, float thr,
-                      const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s);
+void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t f0, int64_t total_strips,
+                      int strip_len, float thr, const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s);
 void launch_landmarks(const uint64_t *mask, const ClipDesc *clips, int n_clips, int64_t total_chunks,
                       int64_t *chunk_counts, uint64_t *records, int64_t *clip_counts, bool write, uint32_t *k2_cold,
                       uint64_t *k2_cold_host, uint32_t k2_waves, bool one_chunk_each, hipStream_t s);
@@ -244,6 +244,7 @@ struct aid_engine {
     int k5_path = 0;       // aid_engine_force K5_PATH: 0 auto, 1 LDS fast path first, 2 global path only (tests)
     int k5_parts = 0;      // aid_engine_force K5_PARTS: K5a key partitions per query (0 = by vote count)
     int lane_gather = 0;           // aid_engine_force LANE_GATHER: stage the exact lane's sub-windows (A/B)
+    int64_t plane_rows = 0;        // aid_engine_force PLANE_ROWS: power rows per K1 -> K2 clip group (0 = kPlaneRows)
     int inject_exchange_fail = 0;  // aid_engine_force EXCHANGE_FAIL: the next exchange's prepare step fails (tests)
     // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
     int64_t st_queries = 0, st_votes = 0, st_post_reads = 0, st_q_global = 0, st_q_lds = 0, st_records = 0;
@@ -562,6 +563,10 @@ int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
             if (value != 0 && value != 1) return fail(AID_ERR_INVALID, "LANE_GATHER: 0 or 1");
             e->lane_gather = value;
             return AID_OK;
+        case AID_FORCE_PLANE_ROWS:
+            if (value < 0) return fail(AID_ERR_INVALID, "PLANE_ROWS must be >= 0");
+            e->plane_rows = value;
+            return AID_OK;
         default:
             return fail(AID_ERR_INVALID, "aid_engine_force: unknown path id");
     }
@@ -573,6 +578,9 @@ int64_t aid_hash_capacity(const aid_engine *e, int64_t n) { return e ? hash_capa
 
 static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc,
                           void *stream, const int64_t *ends = nullptr);
+
+// power rows per K1 -> K2 clip group of one extraction call (3 GB of plane; extract_locked)
+constexpr int64_t kPlaneRows = (int64_t)3 << 18;
 
 int aid_extract(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips, int32_t loc, void *stream) {
     if (!e || !offsets || n_clips < 0) return fail(AID_ERR_INVALID, "aid_extract: bad argument");
@@ -606,8 +614,8 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     // a different stream than the previous call's: order against it the simple way
     if (e->last_stream && e->last_stream != s) HIP_TRY(hipStreamSynchronize(e->last_stream));
     // same clips, PCM location and strip length as the descriptors already on the device: no re-upload
-    const size_t key_n = 2 * (size_t)n_clips + 2;
-    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() == key_n &&
+    // key: [offset, length] per clip, the PCM location, then the K2 strip length of every clip group (below)
+    bool desc_same = e->desc_dev_for_key == e->desc.p && e->desc.p && e->desc_key.size() > 2 * (size_t)n_clips + 1 &&
                      e->desc_key[2 * n_clips] == loc;
     for (int c = 0; desc_same && c < n_clips; ++c)
         desc_same = e->desc_key[2 * c] == offsets[c] && e->desc_key[2 * c + 1] == clip_len(c);
@@ -639,12 +647,41 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
             kx = c >= 0.45 ? 1.5 : c >= 0.3 ? 1.25 : 1.0;
         }
     }
-    const int strip_len = peak_strip_len(e->clip_frames.data(), n_clips, std::max<int64_t>(1, (int64_t)(e->k2_slots * kx)));
-    desc_same = desc_same && e->desc_key[2 * n_clips + 1] == strip_len;  // strip bases depend on the strip length
-    for (int c = 0; c < n_clips; ++c) {
+    // clip groups: consecutive clips whose frames fit kPlaneRows power rows each run K1 -> K2 on one power buffer.
+    // K1 and K2 run 5-14 % slower per audio-second on a 10.8 GB plane than on a 2.7 GB one
+    // (profiles/r05zo_catalog_batch.txt); a call within the bound (the headline's 256 x 10 s, one catalog batch, a
+    // stream push) is one group, as before. K3 runs once over the whole call's mask. AID_FLAG_KEEP_POWER keeps
+    // every row for aid_result_power: one group.
+    std::vector<int> gstart{0};
+    {
+        const bool keep_all = (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0;
+        const int64_t cap = e->plane_rows > 0 ? e->plane_rows : kPlaneRows;
+        int64_t acc = 0;
+        for (int c = 0; c < n_clips; ++c) {
+            if (!keep_all && acc > 0 && acc + e->clip_frames[c] > cap) {
+                gstart.push_back(c);
+                acc = 0;
+            }
+            acc += e->clip_frames[c];
+        }
+        gstart.push_back(n_clips);
+    }
+    const int n_groups = (int)gstart.size() - 1;
+    std::vector<int> glen(n_groups);
+    std::vector<int64_t> gfirst(n_groups), gframes(n_groups, 0), gstrips(n_groups, 0), gk(n_groups, 0);
+    for (int g = 0; g < n_groups; ++g)  // K2 strips per resident slot, per group (strip_base restarts at 0 in each)
+        glen[g] = peak_strip_len(e->clip_frames.data() + gstart[g], gstart[g + 1] - gstart[g],
+                                 std::max<int64_t>(1, (int64_t)(e->k2_slots * kx)));
+    // strip bases follow the groups and their strip lengths: (first clip, strip length) per group in the key
+    desc_same = desc_same && e->desc_key.size() == 2 * (size_t)n_clips + 1 + 2 * (size_t)n_groups;
+    for (int g = 0; desc_same && g < n_groups; ++g)
+        desc_same = e->desc_key[2 * n_clips + 1 + 2 * g] == gstart[g] && e->desc_key[2 * n_clips + 2 + 2 * g] == glen[g];
+    for (int c = 0, g = 0; c < n_clips; ++c) {
         const int64_t n = clip_len(c);
         const int64_t F = num_frames(n, hop);
         ClipDesc &d = e->h_desc[c];
+        while (c == gstart[g + 1]) ++g;
+        if (c == gstart[g]) gfirst[g] = frames;
         if (loc == AID_PCM_DEVICE) {
             d.pcm_off = offsets[c];  // odd: K1's float2 frame loads are then 4-byte aligned (dword alignment suffices)
         } else {
@@ -653,7 +690,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         }
         d.frames = F;
         d.frame_base = frames;
-        d.strip_base = strips;
+        d.strip_base = gstrips[g];  // within the clip's group (K2 runs per group)
         d.chunk_base = chunks;
         d.hash_base = recs;
         d.hash_cap = hash_capacity(F);
@@ -665,13 +702,16 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
         multi_chunk |= nck > 1;
         one_chunk_each &= nck == 1;
         frames += F;
-        strips += (F + strip_len - 1) / strip_len;
+        gframes[g] += F;
+        gstrips[g] += (F + glen[g] - 1) / glen[g];
+        strips += (F + glen[g] - 1) / glen[g];
         chunks += (F + kHashChunk - 1) / kHashChunk;
         recs += d.hash_cap;
+        gk[g] += (F + kStftStrip - 1) / kStftStrip;
         kstrips += (F + kStftStrip - 1) / kStftStrip;
     }
     HIP_TRY(e->desc.reserve((size_t)n_clips + 1));
-    HIP_TRY(e->power.reserve((size_t)frames * kBins));
+    HIP_TRY(e->power.reserve((size_t)std::max<int64_t>(1, *std::max_element(gframes.begin(), gframes.end())) * kBins));
     HIP_TRY(e->mask.reserve((size_t)frames * kMaskWords));
     HIP_TRY(e->hotw.reserve((size_t)frames + 1));
     if (!e->k2_cold.p) {
@@ -709,7 +749,10 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
             e->desc_key[2 * c + 1] = clip_len(c);
         }
         e->desc_key.push_back(loc);
-        e->desc_key.push_back(strip_len);
+        for (int g = 0; g < n_groups; ++g) {
+            e->desc_key.push_back(gstart[g]);
+            e->desc_key.push_back(glen[g]);
+        }
         e->desc_dev_for_key = e->desc.p;
     }
     if (empty_clip || frames == 0) HIP_TRY(hipMemsetAsync(e->counts.p, 0, sizeof(int64_t) * ((size_t)n_clips + 1), s));
@@ -719,20 +762,25 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     e->total_chunks = chunks;
     e->total_records = recs;
     if (frames > 0) {
-        {
-            ProfScope ps(e, AID_K_STFT, s, true);
-            launch_stft_power(dpcm, e->desc.p, n_clips, frames, kstrips, e->k1_slots, hop, e->d_tab, e->power.p, false,
-                              e->hotw.p, e->cfg.peak_threshold, (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0, s);
-        }
-        if (loc == AID_PCM_HOST) {
-            if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(e->stage_ev, s));
-            e->stage_ev_live = true;
-        }
-        {
-            ProfScope ps(e, AID_K_PEAKS, s, true);
-            launch_peak_pick(e->power.p, e->desc.p, n_clips, strips, strip_len, e->cfg.peak_threshold, e->hotw.p,
-                             e->mask.p, e->k2_cold.p, s);
+        for (int g = 0; g < n_groups; ++g) {  // K1 -> K2 per clip group, on one power buffer
+            const int ca = gstart[g], ng = gstart[g + 1] - ca;
+            if (gframes[g] == 0) continue;
+            {
+                ProfScope ps(e, AID_K_STFT, s, true);
+                launch_stft_power(dpcm, e->desc.p + ca, ng, gfirst[g], gframes[g], gk[g], e->k1_slots, hop, e->d_tab,
+                                  e->power.p, false, e->hotw.p, e->cfg.peak_threshold,
+                                  (e->cfg.flags & AID_FLAG_KEEP_POWER) != 0, s);
+            }
+            if (loc == AID_PCM_HOST && g == n_groups - 1) {
+                if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(e->stage_ev, s));
+                e->stage_ev_live = true;
+            }
+            {
+                ProfScope ps(e, AID_K_PEAKS, s, true);
+                launch_peak_pick(e->power.p, e->desc.p + ca, ng, gfirst[g], gstrips[g], glen[g], e->cfg.peak_threshold,
+                                 e->hotw.p, e->mask.p, e->k2_cold.p, s);
+            }
         }
         if (multi_chunk) {  // some clip spans several K3 chunks: their bases need the COUNT pass
             ProfScope ps(e, AID_K_LANDMARK_COUNT, s, true);
@@ -847,7 +895,7 @@ int aid_spectrogram(aid_engine *e, const float *pcm, int64_t n, float *out, int6
     if (he == hipSuccess) he = hipMemcpy(d_pcm, pcm, n * sizeof(float), hipMemcpyHostToDevice);
     if (he == hipSuccess) he = hipMemcpy(d_desc, &d, sizeof(ClipDesc), hipMemcpyHostToDevice);
     if (he == hipSuccess) {
-        launch_stft_power(d_pcm, d_desc, 1, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
+        launch_stft_power(d_pcm, d_desc, 1, 0, F, (F + kStftStrip - 1) / kStftStrip, e->k1_slots, e->cfg.hop, e->d_tab,
                           d_out, true, nullptr, e->cfg.peak_threshold, true, s);
         he = hipGetLastError();
     }

@@ -65,7 +65,7 @@ __device__ __forceinline__ int pkey(float x) {
 
 // occupancy 4 forced by the launch bounds (<= 128 VGPRs, no spills)
 __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
-                                                  int n_clips, int64_t total_strips, int strip_len, float thr,
+                                                  int n_clips, int64_t f0, int64_t total_strips, int strip_len, float thr,
                                                   const uint64_t *__restrict__ hot, uint64_t *__restrict__ mask,
                                                   uint32_t *__restrict__ cold_cnt) {
     __shared__ __attribute__((aligned(16))) int rows[kRowsPerStep][kBins + 32];  // keys, 16 pads each side
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
     const int64_t fb = clips[lo].frame_base;
     const int t0 = (int)(strip - clips[lo].strip_base) * strip_len;
     const int t1 = min(t0 + strip_len, F);
-    const float *P = power + fb * kBins;
+    const float *P = power + (fb - f0) * kBins;  // the plane holds rows from absolute frame f0 on
     uint64_t *M = mask + fb * kMaskWords + 4 * wave + lane;  // lanes 0..3 store ballot words
     // K1's plane holds Q = 4P (stft.hip, real split): compare against 4 thr (exact: thr <= 2^100)
     const int kthr = __float_as_int(4.0f * thr);            // thr > 0 (engine config check)
@@ -349,10 +349,12 @@ int k2_stamps_read(unsigned long long *out, bool reset) {
 }
 #endif
 
-void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t total_strips, int strip_len,
-                      float thr, const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {
+// power holds the rows from absolute frame f0 on (a group of the call's clips, extract_locked); the clips' strip_base
+// count from 0 within the group
+void launch_peak_pick(const float *power, const ClipDesc *clips, int n_clips, int64_t f0, int64_t total_strips,
+                      int strip_len, float thr, const uint64_t *hot, uint64_t *mask, uint32_t *cold_cnt, hipStream_t s) {
     if (total_strips <= 0) return;
-    timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, total_strips,
+    timed_launch(k_peak_pick, dim3((unsigned)total_strips), dim3(256), 0, s, power, clips, n_clips, f0, total_strips,
                  strip_len, thr, hot, mask, cold_cnt);
 }
 

@@ -100,7 +100,7 @@ __device__ __forceinline__ int e3q_slot(int k) { return 4 * (k & 255) + ((k >> 8
 template <bool LOGMAG, int ROWS>
 __global__ __launch_bounds__(kStftWaves * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_stft_power(const float *__restrict__ pcm,
                                                                 const ClipDesc *__restrict__ clips, int n_clips,
-                                                                int64_t total, int64_t n_waves,
+                                                                int64_t f0, int64_t total, int64_t n_waves,
                                                                 const Tables *__restrict__ tab, float *__restrict__ out,
                                                                 uint64_t *__restrict__ hot, float thr, int keep) {
     constexpr int PERIOD = 16 / ROWS;  // frames per full ring rotation
@@ -164,8 +164,9 @@ __global__ __launch_bounds__(kStftWaves * 64) __attribute__((amdgpu_waves_per_eu
     // the same work (no partial last round), and a segment restarts the ring only at a clip edge
     const int64_t g = (int64_t)blockIdx.x * kStftWaves + wave;
     if (g >= n_waves) return;  // wave-uniform, after the only barrier
-    int64_t f = g * total / n_waves;
-    const int64_t f_end = (g + 1) * total / n_waves;
+    // frames [f0, f0 + total) of the call (a group of its clips, extract_locked); out holds rows from f0 on
+    int64_t f = f0 + g * total / n_waves;
+    const int64_t f_end = f0 + (g + 1) * total / n_waves;
     while (f < f_end) {
     int lo = 0, hi = n_clips - 1;
     while (lo < hi) {  // last clip with frame_base <= f (scalar loads): the clip holding frame f
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(kStftWaves * 64) __attribute__((amdgpu_waves_per_eu
     const int64_t t0 = f - clips[lo].frame_base;
     const int nfr = (int)min(f_end - f, clips[lo].frames - t0);
     const aid_f2u *src = reinterpret_cast<const aid_f2u *>(pcm + clips[lo].pcm_off) + t0 * HOP2 + e1_perm(lane);
-    float *dst = out + (clips[lo].frame_base + t0) * kBins;
+    float *dst = out + (clips[lo].frame_base - f0 + t0) * kBins;
     uint64_t *dhot = LOGMAG ? nullptr : hot + clips[lo].frame_base + t0;
 
     float2 ring[16];
@@ -450,19 +451,20 @@ __global__ __launch_bounds__(kStftWaves * 64) __attribute__((amdgpu_waves_per_eu
 
 template <bool LOGMAG>
 static void launch_rows(int rows, dim3 g, dim3 b, hipStream_t s, const float *pcm, const ClipDesc *clips, int n_clips,
-                        int64_t total, int64_t n_waves, const Tables *tab, float *out, uint64_t *hot, float thr, int keep) {
+                        int64_t f0, int64_t total, int64_t n_waves, const Tables *tab, float *out, uint64_t *hot, float thr,
+                        int keep) {
     switch (rows) {
-        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
-        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, thr, keep); break;
+        case 1: timed_launch((k_stft_power<LOGMAG, 1>), g, b, 0, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, hot, thr, keep); break;
+        case 2: timed_launch((k_stft_power<LOGMAG, 2>), g, b, 0, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, hot, thr, keep); break;
+        case 4: timed_launch((k_stft_power<LOGMAG, 4>), g, b, 0, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, hot, thr, keep); break;
+        case 8: timed_launch((k_stft_power<LOGMAG, 8>), g, b, 0, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, hot, thr, keep); break;
+        default: timed_launch((k_stft_power<LOGMAG, 16>), g, b, 0, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, hot, thr, keep); break;
     }
 }
 
-// total_frames = sum of the clips' frames, total_strips = sum of ceil(F / kStftStrip) (strip mode),
-// slots = resident K1 waves on the device (CUs x kStftWaves)
-void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t total_frames,
+// total_frames = sum of the clips' frames, the first at absolute frame f0 (out = its power row),
+// total_strips = sum of ceil(F / kStftStrip) (strip mode), slots = resident K1 waves on the device (CUs x kStftWaves)
+void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int64_t f0, int64_t total_frames,
                        int64_t total_strips, int64_t slots, int hop, const Tables *tab, float *out, bool logmag,
                        uint64_t *hot, float thr, bool keep_power, hipStream_t s) {
     if (total_frames <= 0) return;
@@ -473,9 +475,9 @@ void launch_stft_power(const float *pcm, const ClipDesc *clips, int n_clips, int
         1, total_frames >= slots * kStftStrip ? slots : std::min<int64_t>(slots, total_frames / kK1MinFrames));
     const int64_t total = total_frames;
     const dim3 g((unsigned)((n_waves + kStftWaves - 1) / kStftWaves)), b(kStftWaves * 64);
-    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, nullptr, thr, 1);
+    if (logmag) launch_rows<true>(hop / 128, g, b, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, nullptr, thr, 1);
     else  // the power plane holds 4P (see the real split): hot blocks are those with 4P > 4 thr
-        launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, total, n_waves, tab, out, hot, 4.0f * thr,
+        launch_rows<false>(hop / 128, g, b, s, pcm, clips, n_clips, f0, total, n_waves, tab, out, hot, 4.0f * thr,
                            keep_power ? 1 : 0);
 }
 

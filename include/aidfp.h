@@ -104,6 +104,8 @@ int aid_engine_config(const aid_engine *e, aid_config *out);
                                       aid_index_allgather) fails with AID_ERR_NOMEM, once (rank-failure tests) */
 #define AID_FORCE_LANE_GATHER 7    /* 1: aid_exact_lane copies its sub-windows to a staging buffer before K1 instead
                                       of extracting them in place (A/B) */
+#define AID_FORCE_PLANE_ROWS 8     /* 0 default (786,432), else power rows per K1 -> K2 clip group of one extraction
+                                      call (tests: small calls split into several groups) */
 int aid_engine_force(aid_engine *e, int32_t what, int32_t value);
 
 /* Frames and worst-case record count of a clip of n samples (FPSPEC 1, 5). */

@@ -108,6 +108,23 @@ def test_device_pcm_and_many_clips(service):
         assert np.array_equal(a[i], b[i]) and np.array_equal(a[i], ref[i % len(base)])
 
 
+def test_lane_rows_under_clip_groups(service):
+    """The lane's windows split into several K1 -> K2 groups (engine.cpp extract_locked; `plane_rows` forces a
+    small bound) give the same rows as one group."""
+    base = clips()[3:12]
+    many = [base[i % len(base)] for i in range(120)]
+    eng = service._engine
+    ref = eng.exact_lane(many)
+    try:
+        for rows in (300, 5000):
+            eng.force("plane_rows", rows)
+            got = eng.exact_lane(many)
+            for i in range(len(many)):
+                assert np.array_equal(got[i], ref[i]), f"plane_rows {rows}, clip {i}: rows differ"
+    finally:
+        eng.force("plane_rows", 0)
+
+
 def test_single_clip_default_path(service):
     fp.set_service(service)
     try:

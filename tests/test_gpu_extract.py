@@ -303,3 +303,32 @@ def test_k2_strip_multipliers_bit_exact(slots_x):
             pk = peaks_from_mask(eng.peakmask(c, len(x)))
             assert np.array_equal(pk, O.peaks(O.stft_power(x, HOP)).reshape(-1, 2)), f"clip {c}: peaks differ"
             assert np.array_equal(got[c], O.fingerprint(x, HOP)), f"clip {c}: hashes differ"
+
+
+@pytest.mark.parametrize("rows", [0, 1, 700, 2000])
+def test_clip_groups_bit_exact(rows):
+    """A call whose frames exceed the plane bound runs K1 -> K2 per group of clips on one power buffer (engine.cpp
+    extract_locked, kPlaneRows; `plane_rows` forces the bound). Every grouping gives the oracle's peaks and hashes:
+    a group per clip (1), several clips per group with a clip longer than the bound alone in its group (700, 2000
+    rows; the 40 s clip has 3,445 frames), and one group (0); host and device PCM, and calls repeated (cached
+    descriptors keyed on the groups)."""
+    import torch
+
+    from aidfp.engine import Engine
+
+    lens = [44100 * 4 + 313 * t for t in range(9)] + [44100 * 40, 100, 44100 * 3]
+    clips = [_clip(t, n, snr=None if t % 3 else 20) for t, n in enumerate(lens)]
+    refs = [O.fingerprint(x, HOP) for x in clips]
+    with Engine(SR) as eng:
+        eng.force("plane_rows", rows)
+        for _ in range(2):
+            got = eng.extract_host(clips)
+            for c, x in enumerate(clips):
+                pk = peaks_from_mask(eng.peakmask(c, len(x)))
+                assert np.array_equal(pk, O.peaks(O.stft_power(x, HOP)).reshape(-1, 2)), f"clip {c}: peaks differ"
+                assert np.array_equal(got[c], refs[c]), f"clip {c}: hashes differ"
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        dev = torch.from_numpy(np.concatenate(clips).astype(np.float32)).cuda()
+        eng.extract_device(dev.data_ptr(), offs)
+        for c in range(len(clips)):
+            assert np.array_equal(eng.hashes(c), refs[c]), f"device PCM, clip {c}: hashes differ"
