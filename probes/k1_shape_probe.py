@@ -4,7 +4,7 @@ steps against the catalog leg's 1,024 x 30 s batches, same generator, same box, 
 shape is generated once and extracted repeatedly for ~--seconds of device time; the shapes are interleaved over
 --rounds so clock or thermal drift shows up as a trend rather than as a shape effect. Diagnostic only.
 
-    python probes/k1_shape_probe.py [--rounds 3] [--seconds 1.5]
+    python probes/k1_shape_probe.py [--rounds 3] [--seconds 1.5] [--plane-rows R]
 """
 import argparse
 import json
@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=1.5)
     ap.add_argument("--shapes", default="256x10,1024x30,256x30,1024x10")
+    ap.add_argument("--plane-rows", type=int, default=0,
+                    help="power rows per K1 -> K2 clip group (aid_engine_force PLANE_ROWS; 0 = the engine's 3 GB default)")
     args = ap.parse_args()
     import torch
 
@@ -31,6 +33,8 @@ def main():
     sr = 44100
     torch.cuda.set_device(0)
     eng = Engine(sr, device=0)
+    if args.plane_rows:
+        eng.force("plane_rows", args.plane_rows)
     shapes = [tuple(int(v) for v in s.split("x")) for s in args.shapes.split(",")]
     bufs = {}
     for clips, secs in shapes:
@@ -58,7 +62,8 @@ def main():
             wall = time.perf_counter() - t0
             k = eng.profile_read(reset=True)
             per = {name: round(1e3 * ms / (reps * audio / 1000.0), 2) for name, (ms, cnt) in k.items() if cnt}
-            print(json.dumps({"round": r, "clips": shape[0], "seconds": shape[1], "launches": reps,
+            print(json.dumps({"round": r, "clips": shape[0], "seconds": shape[1], "plane_rows": args.plane_rows,
+                              "launches": reps,
                               "us_per_1000_audio_s": per, "wall_audio_s_per_s": round(reps * audio / wall, 1)}),
                   flush=True)
     eng.close()
