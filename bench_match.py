@@ -43,6 +43,8 @@ def main() -> int:
     ap.add_argument("--no-cpu", action="store_true", help="skip the host-oracle baseline")
     ap.add_argument("--cpu-tracks", type=int, default=1000, help="index size of the host baseline (extrapolated)")
     ap.add_argument("--cpu-clips", type=int, default=192, help="query clips of the host baseline")
+    ap.add_argument("--plane-rows", type=int, default=0,
+                    help="diagnostic: power rows per K1 -> K2 clip group (aid_engine_force PLANE_ROWS; 0 = default)")
     args = ap.parse_args()
 
     import torch
@@ -55,6 +57,8 @@ def main() -> int:
 
     torch.cuda.set_device(0)
     eng = Engine(args.sr, device=0, min_match=args.min_match)
+    if args.plane_rows:
+        eng.force("plane_rows", args.plane_rows)
     t0 = time.perf_counter()
     st = ingest_synthetic(eng, np.arange(args.tracks, dtype=np.uint32), args.seconds)
     t_index = time.perf_counter() - t0
