@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=1.5)
     ap.add_argument("--shapes", default="256x10,1024x30,256x30,1024x10")
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="sync and sleep this long after every extraction call (0 = calls back to back)")
     ap.add_argument("--plane-rows", type=int, default=0,
                     help="power rows per K1 -> K2 clip group (aid_engine_force PLANE_ROWS; 0 = the engine's 3 GB default)")
     args = ap.parse_args()
@@ -54,6 +56,9 @@ def main():
             while True:
                 eng.extract_device(pcm.data_ptr(), offs)
                 reps += 1
+                if args.gap_ms > 0:
+                    eng.sync()
+                    time.sleep(args.gap_ms * 1e-3)
                 if reps % 4 == 0:
                     eng.sync()
                     if time.perf_counter() - t0 > args.seconds:
@@ -63,6 +68,7 @@ def main():
             k = eng.profile_read(reset=True)
             per = {name: round(1e3 * ms / (reps * audio / 1000.0), 2) for name, (ms, cnt) in k.items() if cnt}
             print(json.dumps({"round": r, "clips": shape[0], "seconds": shape[1], "plane_rows": args.plane_rows,
+                              "gap_ms": args.gap_ms,
                               "launches": reps,
                               "us_per_1000_audio_s": per, "wall_audio_s_per_s": round(reps * audio / wall, 1)}),
                   flush=True)
