@@ -76,6 +76,10 @@ def build(verbose: bool = False, variant: str | None = None, defines: tuple = ()
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    # hipcc's shared link can leave per-object offload bundles (<lib>.N.hipv4-..., <lib>.N.host-...) beside the
+    # library: intermediates, never loaded
+    for junk in list(lib.parent.glob(lib.name + ".*.hipv4-*")) + list(lib.parent.glob(lib.name + ".*.host-*")):
+        junk.unlink()
     return lib
 
 
