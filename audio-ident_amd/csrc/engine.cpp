@@ -49,6 +49,7 @@ void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint
                           const uint8_t *tomb, uint32_t n_tracks, uint32_t *cursor, uint64_t *post, hipStream_t s);
 void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
 size_t index_sort_temp_bytes(int64_t n);
+bool k4_ab_sort_built();
 size_t radix_scratch_u32(int64_t n);
 hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
@@ -69,7 +70,7 @@ void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
-                  int parts, int stage, hipStream_t s);
+                  int parts, int stage, uint32_t *dset, int dset_bits, hipStream_t s);
 void launch_count_nonzero(const uint32_t *cnt, int64_t n, unsigned long long *out, hipStream_t s);
 void launch_index_checksum(const uint32_t *ph, const uint32_t *ptr, const uint32_t *pt, int64_t first, int64_t n,
                            unsigned long long *out, hipStream_t s);
@@ -189,7 +190,8 @@ struct aid_engine {
     DevBuf<uint64_t> srt_v;           // K4 sort build: the value buffer idx_post pairs with
     DevBuf<uint8_t> srt_tmp;          // K4 rocPRIM build (A/B): its temporary storage
     DevBuf<uint32_t> srt_scratch;     // K4 radix build: per-tile digit counts, their scan, scan temporary
-    int k4_mode = 2;                  // aid_engine_force K4_BUILD: 2 radix sort (default), 1 rocPRIM sort, 0 atomic
+    int k4_mode = 2;                  // internal K4 build: 2 radix sort (the default; K4_BUILD force 0, 1 or 4),
+                                      // 1 rocPRIM sort (force 3, variant build only), 0 atomic counting sort (force 2)
     int k4_rank = 0;                  // radix sort's in-wave rank: 0 one LDS atomic per posting where the device
                                       // serves same-address lanes in order (else ballots), 1 ballots (K4_BUILD 4)
     bool index_built = false, index_dirty = true;
@@ -204,6 +206,7 @@ struct aid_engine {
     DevBuf<uint32_t> q_hist;
     DevBuf<int32_t> q_rows, q_nrows;
     DevBuf<uint32_t> q_hot;  // K5h hot-bucket bitmaps, [batch][2^bits / 32]
+    DevBuf<uint32_t> q_dset;  // K5b retries: HBM distinct (slot, t_q) sets, [batch][2^dbits]
     DevBuf<int64_t> q_votes;  // exact votes per query (LDS-histogram eligibility)
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
@@ -354,7 +357,7 @@ int aid_config_default(int32_t sample_rate, aid_config *out) {
     out->hop = sample_rate >= 32000 ? 512 : 256;
     out->peak_threshold = 4.0f;
     out->device = -1;
-    out->min_match = 12;
+    out->min_match = 10;
     out->max_results = 50;
     return AID_OK;
 }
@@ -372,7 +375,7 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
     // any Q of a candidate (Q > 4 thr) is normal, so Q-order and P-order decide every comparison alike
     if (!(c.peak_threshold >= 0x1p-124f) || c.peak_threshold > 0x1p100f)
         return fail(AID_ERR_INVALID, "peak_threshold must be in [2^-124, 2^100]");
-    if (c.min_match <= 0) c.min_match = 12;
+    if (c.min_match <= 0) c.min_match = 10;
     if (c.max_results <= 0) c.max_results = 50;
     if (c.flags & ~AID_FLAG_KEEP_POWER) return fail(AID_ERR_INVALID, "unknown aid_config.flags bits");
     int ndev = 0;
@@ -437,6 +440,9 @@ int aid_engine_create(const aid_config *cfg, aid_engine **out) {
 
 void aid_engine_destroy(aid_engine *e) {
     if (!e) return;
+    // a call still running on another thread (ctypes releases the GIL) holds e->mu: it finishes before anything
+    // is freed; the lock is released before the engine itself is deleted below
+    std::unique_lock<std::mutex> destroy_lk(e->mu);
     (void)hipSetDevice(e->device);
     if (e->own_stream) (void)hipStreamSynchronize(e->own_stream);
     (void)hipDeviceSynchronize();
@@ -476,6 +482,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->q_count.release();
     e->q_hist.release();
     e->q_hot.release();
+    e->q_dset.release();
     e->q_rows.release();
     e->q_nrows.release();
     e->x_src.release();
@@ -518,6 +525,7 @@ void aid_engine_destroy(aid_engine *e) {
     if (e->d_tab) (void)hipFree(e->d_tab);
     if (e->d_sin) (void)hipFree(e->d_sin);
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    destroy_lk.unlock();
     delete e;
 }
 
@@ -551,6 +559,9 @@ int aid_engine_force(aid_engine *e, int32_t what, int32_t value) {
         case AID_FORCE_K4_BUILD:
             if (value < 0 || value > 4)
                 return fail(AID_ERR_INVALID, "K4_BUILD: 0 default, 1 radix, 2 atomic, 3 rocPRIM, 4 radix with ballot ranks");
+            if (value == 3 && !k4_ab_sort_built())
+                return fail(AID_ERR_INVALID, "K4_BUILD 3: the rocPRIM A/B build is only in the diagnostic variant "
+                                             "library (build_ext.build(variant=\"k4rocprim\"), -DAID_K4_ROCPRIM_AB)");
             e->k4_mode = value == 2 ? 0 : value == 3 ? 1 : 2;
             e->k4_rank = value == 4 ? 1 : 0;
             e->index_dirty = true;
@@ -924,15 +935,16 @@ int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int6
     const bool async = (flags & AID_SYNTH_ASYNC) != 0;
     // the engine's last work on another stream may still read dst; on the same stream it is ordered already
     if (e->last_stream && (!async || e->last_stream != s)) HIP_TRY(hipStreamSynchronize(e->last_stream));
-    HIP_TRY(e->synth_tracks.reserve(n_clips));
-    HIP_TRY(e->synth_starts.reserve(n_clips));
-    // tracks + starts go up from pinned staging (the caller's arrays may be gone when an async copy runs); the
-    // previous call's copies must have left it
-    const size_t tb = ((size_t)n_clips * sizeof(uint32_t) + 7) & ~(size_t)7, need = tb + (size_t)n_clips * sizeof(int64_t);
+    // the previous call's copies and kernel must have left the pinned staging and the device arrays before a
+    // reserve may reallocate them or the copies below overwrite them
     if (e->synth_ev_live) {
         HIP_TRY(hipEventSynchronize(e->synth_ev));
         e->synth_ev_live = false;
     }
+    HIP_TRY(e->synth_tracks.reserve(n_clips));
+    HIP_TRY(e->synth_starts.reserve(n_clips));
+    // tracks + starts go up from pinned staging (the caller's arrays may be gone when an async copy runs)
+    const size_t tb = ((size_t)n_clips * sizeof(uint32_t) + 7) & ~(size_t)7, need = tb + (size_t)n_clips * sizeof(int64_t);
     if (need > e->h_synth_cap) {
         if (e->h_synth) HIP_TRY(hipHostFree(e->h_synth));
         e->h_synth = nullptr;
@@ -944,15 +956,19 @@ int aid_synth_rate(aid_engine *e, float *dst, const uint32_t *tracks, const int6
     std::memcpy(e->h_synth + tb, starts, (size_t)n_clips * sizeof(int64_t));
     HIP_TRY(hipMemcpyAsync(e->synth_tracks.p, e->h_synth, n_clips * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(e->synth_starts.p, e->h_synth + tb, n_clips * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    if (!e->synth_ev) HIP_TRY(hipEventCreateWithFlags(&e->synth_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(e->synth_ev, s));
-    e->synth_ev_live = true;
     {
         ProfScope ps(e, AID_K_SYNTH, s);
         launch_synth(dst, e->synth_tracks.p, e->synth_starts.p, n_clips, n, sample_rate, noise_a, salt, fmax_hz,
                      !(flags & AID_SYNTH_STATIONARY), e->d_sin, s);
     }
     HIP_TRY(hipGetLastError());
+    // the event covers the kernel's reads of synth_tracks / synth_starts as well as the copies into them, so the
+    // next call (any stream) waits for both before it reuses the pinned staging or the device arrays; last_stream
+    // makes every later call on another stream wait for this one too
+    if (!e->synth_ev) HIP_TRY(hipEventCreateWithFlags(&e->synth_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(e->synth_ev, s));
+    e->synth_ev_live = true;
+    e->last_stream = s;
     if (!async) HIP_TRY(hipStreamSynchronize(s));
     return AID_OK;
 }
@@ -2107,7 +2123,8 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // 185k clips/s, rows equal), so a batch goes to it when its mean query has <= 2^17 votes (2 per counter) and
     // none has more than 2^20 (a heavier one falls back to the global path after its LDS run)
     // Each query is routed by its own vote count: k_match_lds answers the queries with <= kLdsMaxVotes
-    // (2 per 16-bit-indexed counter) and hands heavier ones straight back (nrows -1, no LDS run), so the batch takes
+    // (2^18 votes over the 2^15 8-bit counters of its filter = 8 per counter, aidfp_layout.h) and hands heavier ones
+    // straight back (nrows -1, no LDS run), so the batch takes
     // the LDS launch whenever some query is light enough for it; the heavy ones run on the global path below
     int n_light = 0;
     for (int q = 0; q < nq; ++q) n_light += h_votes[q] <= kLdsMaxVotes;
@@ -2168,14 +2185,25 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             out_n = out_rows + (size_t)order.size() * mr * 5;
         }
         const int n = (int)order.size();
-        for (int q0 = 0; q0 < n; q0 += batch) {
-            const int nb = std::min(batch, n - q0);
+        // from the second global attempt on, the distinct (slot, t_q) sets live in HBM (2^dbits entries per query,
+        // 4x more per attempt): a query that overflowed k_vote_final's LDS set is a long one with a strong match
+        // (FPSPEC v1 7), which more histogram buckets do not help
+        const int dbits = attempt >= 2 ? std::min(12 + 2 * attempt, 26) : 0;
+        int dbatch = batch;
+        if (dbits) {
+            dbatch = (int)std::max<size_t>(1, std::min<size_t>((size_t)batch, ((size_t)1 << 30) / ((size_t)4 << dbits)));
+            HIP_TRY(e->q_dset.reserve((size_t)std::min(dbatch, n) << dbits));
+        }
+        for (int q0 = 0; q0 < n; q0 += dbatch) {
+            const int nb = std::min(dbatch, n - q0);
+            if (dbits) HIP_TRY(hipMemsetAsync(e->q_dset.p, 0xFF, ((size_t)nb << dbits) * sizeof(uint32_t), s));
             // K5a, K5h, K5b, each with its own dispatch-attached events when profiled
             for (int stage = 1; stage <= 3; ++stage) {
                 ProfScope ps(e, stage == 1 ? AID_K_VOTE_HIST : stage == 2 ? AID_K_HOT_SCAN : AID_K_VOTE_FINAL, s, true);
                 launch_query(recs, qs + q0, qc + q0, nb, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_hist.p, bits, e->q_hot.p, out_rows + (size_t)q0 * mr * 5,
-                             out_n + q0, e->tomb_since_build > 0, parts, stage, s);
+                             out_n + q0, e->tomb_since_build > 0, parts, stage, dbits ? e->q_dset.p : nullptr, dbits,
+                             s);
             }
             HIP_TRY(hipGetLastError());
         }
@@ -2207,6 +2235,16 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     return AID_OK;
 }
 
+// K5 keys its distinct-frame sets by (table slot << 20 | t_q) (index.hip distinct_first): a query's anchor frames must
+// stay below 2^20 - 1 (3.4 h of audio at 44.1 kHz, 4.6 h at 16 kHz)
+constexpr int64_t kMaxQueryFrame = ((int64_t)1 << 20) - 2;
+static int check_query_frames(const aid_engine *e) {
+    for (int c = 0; c < e->n_clips; ++c)
+        if (e->clip_frames[c] > kMaxQueryFrame + 1)
+            return fail(AID_ERR_INVALID, "query clip longer than 2^20 - 1 frames (FPSPEC v1 7)");
+    return AID_OK;
+}
+
 static int ensure_index(aid_engine *e) {
     if (e->index_dirty || !e->index_built) return finalize_locked(e);
     return AID_OK;
@@ -2218,6 +2256,9 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
     if (nq == 0) return AID_OK;
     for (int q = 0; q < nq; ++q)
         if (qoff[q + 1] < qoff[q]) return fail(AID_ERR_INVALID, "aid_query: offsets must be non-decreasing");
+    for (int64_t i = qoff[0]; i < qoff[nq]; ++i)
+        if ((int64_t)recs[i].t1 > kMaxQueryFrame)
+            return fail(AID_ERR_INVALID, "aid_query: record anchor frame >= 2^20 - 1 (FPSPEC v1 7)");
     std::lock_guard<std::mutex> lk(e->mu);
     if (int rc = ensure_index(e)) return rc;
     hipStream_t s = e->own_stream;
@@ -2239,6 +2280,7 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
 }
 
 static int query_extracted_locked(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
+    if (int rc = check_query_frames(e)) return rc;
     if (int rc = ensure_index(e)) return rc;
     hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
     const int nq = e->n_clips;
@@ -2408,6 +2450,7 @@ static int exact_lane_locked(aid_engine *e, const float *pcm, const int64_t *off
         } else {
             if (int rc = extract_locked(e, src, wstart.data(), n_win, AID_PCM_DEVICE, s, wend.data())) return rc;
         }
+        if (int rc = check_query_frames(e)) return rc;
         HIP_TRY(e->q_start.reserve(n_win));
         HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), n_win * sizeof(int64_t), hipMemcpyHostToDevice, s));
         if (int rc = run_queries(e, e->records.p, e->q_start.p, e->counts.p, n_win, -1, nullptr, nrows.data(), s))

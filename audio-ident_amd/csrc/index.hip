@@ -35,6 +35,8 @@ constexpr int kTrackCap = 1024;  // LDS per-track best entries per query
 // the query is re-run on more buckets (still exact). Probing a full 4096-slot table per vote had
 // made an overflowing query cost ~100x a normal one.
 constexpr int kProbeMax = 512;
+constexpr int kDistinctBits = 13;  // k_vote_final's (slot, t_q) set in LDS (32 KB, shared with its row staging)
+constexpr int kDistinctCap = 1 << kDistinctBits;
 constexpr int kHotLdsBits = 17;  // K5b stages hot bitmap rows of up to 2^17 bits (16 KB) in LDS
 
 __device__ __forceinline__ uint32_t key26(uint32_t h) { return bucket_key(h); }  // aidfp_layout.h
@@ -45,6 +47,24 @@ __device__ __forceinline__ uint32_t mix_td(uint32_t track, int32_t d) {
     x *= 0x2C1B3C6Du;
     x ^= x >> 12;
     return x;
+}
+
+// FPSPEC v1 7: a (track, d) scores the DISTINCT query anchor frames among its votes. The exact tables count a vote
+// only when its (table slot, t_q) pair is new: an open-addressed LDS set of (slot << 20 | t_q) keys (t_q < 2^20 - 1,
+// host-checked), whose first insert of a key returns true. A full set (more probes than entries) reports overflow:
+// the query is answered again on a larger table, as for the (track, d) tables themselves.
+constexpr uint32_t kDistinctEmpty = 0xFFFFFFFFu;
+__device__ __forceinline__ bool distinct_first(uint32_t *set, int bits, uint32_t slot, uint32_t tq, int32_t *overflow) {
+    const uint32_t key = (slot << 20) | tq, mask = (1u << bits) - 1;
+    uint32_t i = (key * 0x9E3779B1u) >> (32 - bits);
+    for (uint32_t probes = 0; probes <= mask; ++probes) {
+        const uint32_t old = atomicCAS(&set[i], kDistinctEmpty, key);
+        if (old == kDistinctEmpty) return true;
+        if (old == key) return false;
+        i = (i + 1) & mask;
+    }
+    *overflow = 1;
+    return false;
 }
 
 // ---- K4: build ----
@@ -255,6 +275,9 @@ struct QueryParams {
     int32_t parts;             // K5a workgroups (key partitions) per query
     const int64_t *votes;      // [nq] exact votes per query (k_query_votes, earlier on the stream); LDS path only
     const uint16_t *sig;       // [n] 2-B vote signature per posting (aidfp_layout.h posting_sig); LDS path only
+    uint32_t *dset;            // K5b: [nq][2^dset_bits] distinct (slot, t_q) sets in HBM, all kDistinctEmpty on entry
+                               // (a retry of queries whose LDS set overflowed); nullptr = the LDS set
+    int32_t dset_bits;
 };
 
 // Every vote (track, d = t_ref - t_q, t_q) of query records [a, a + n), for the calling wave's
@@ -444,7 +467,12 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
     __shared__ unsigned long long tbest[kTrackCap];    // count << 32 | ~(d + 2^31)
     __shared__ int32_t out_n;
     __shared__ int32_t overflow;
-    __shared__ int32_t rowbuf[kTrackCap][5];
+    // the distinct-frame set of the insert phase and the row staging of the output phase share their LDS
+    __shared__ union {
+        uint32_t dset[kDistinctCap];
+        int32_t rowbuf[kTrackCap][5];
+    } ur;
+    int32_t(*rowbuf)[5] = ur.rowbuf;
     __shared__ uint32_t hotl[1 << (kHotLdsBits - 5)];
     const int q = blockIdx.x;
     const int tid = threadIdx.x;
@@ -458,6 +486,12 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
         tkey[i] = 0xFFFFFFFFu;
         tbest[i] = 0ull;
     }
+    // the set of distinct (slot, t_q): in LDS, or (a retry of a query whose LDS set overflowed: long queries with
+    // strong matches) a larger one in HBM that the host filled with kDistinctEmpty
+    uint32_t *dset = qp.dset ? qp.dset + ((int64_t)blockIdx.x << qp.dset_bits) : ur.dset;
+    const int dbits = qp.dset ? qp.dset_bits : kDistinctBits;
+    if (!qp.dset)
+        for (int i = tid; i < kDistinctCap; i += blockDim.x) ur.dset[i] = kDistinctEmpty;
     if (tid == 0) { out_n = 0; overflow = 0; }
     __syncthreads();
     const int64_t a = qp.qstart[q], z = a + qp.qcount[q];
@@ -480,7 +514,7 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
         for (;;) {
             const unsigned long long old = atomicCAS(&vkey[s], ~0ull, key);
             if (old == ~0ull || old == key) {
-                atomicAdd(&vcnt[s], 1u);
+                if (distinct_first(dset, dbits, s, (uint32_t)tq, &overflow)) atomicAdd(&vcnt[s], 1u);
                 atomicMin(&vmin[s], (uint32_t)tq);
                 atomicMax(&vmax[s], (uint32_t)tq);
                 break;
@@ -586,7 +620,11 @@ constexpr int kLdsHistBits = 15;
 constexpr int kLdsCtrBits = 8;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
-constexpr int kFastVoteCap = 1024;
+// (track, d) entries of the exact table: the music-like and synthetic catalogs hold <= 86 per window
+// (probes/spec_sweep.py statistics); a fuller table overflows to the global path
+constexpr int kFastVoteCap = 512;
+constexpr int kFastDistinctBits = 10;  // the (slot, t_q) set: <= 615 distinct per window on the same data
+constexpr int kFastDistinctCap = 1 << kFastDistinctBits;
 constexpr int kFastTrackCap = 512;
 constexpr int kFastThreads = 512;
 
@@ -732,7 +770,7 @@ __device__ __forceinline__ void sig_votes(const QueryParams &qp, int64_t a, int6
 }
 
 // hot votes queued by the insert pass (posting index, tq): the LDS the counters leave beside the exact table
-constexpr int kTableBytes = kFastVoteCap * (8 + 3 * 4) + kFastTrackCap * (4 + 8);
+constexpr int kTableBytes = kFastVoteCap * (8 + 3 * 4) + kFastTrackCap * (4 + 8) + kFastDistinctCap * 4;
 constexpr int kHotQueue = ((1 << kLdsHistBits) / kLdsCtrPerWord * 4 - kTableBytes) / 8;
 
 struct FastLds {
@@ -743,6 +781,7 @@ struct FastLds {
             uint32_t vcnt[kFastVoteCap], vmin[kFastVoteCap], vmax[kFastVoteCap];
             uint32_t tkey[kFastTrackCap];
             unsigned long long tbest[kFastTrackCap];
+            uint32_t dset[kFastDistinctCap];  // distinct (slot, t_q) of the inserted votes
             uint2 hq[kHotQueue > 0 ? kHotQueue : 1];  // the insert pass's hot votes (posting index, tq)
         } t;
     } u;
@@ -829,6 +868,7 @@ void k_match_lds(QueryParams qp) {
         L.u.t.tkey[i] = 0xFFFFFFFFu;
         L.u.t.tbest[i] = 0ull;
     }
+    for (int i = tid; i < kFastDistinctCap; i += kFastThreads) L.u.t.dset[i] = kDistinctEmpty;
     __syncthreads();
     // the exact (track, d) table insert of one hot vote (slot from the full mix of (track, d))
     auto insert = [&](uint32_t tr, int32_t d, int32_t tq) {
@@ -838,7 +878,8 @@ void k_match_lds(QueryParams qp) {
         for (;;) {
             const unsigned long long old = atomicCAS(&L.u.t.vkey[s], ~0ull, key);
             if (old == ~0ull || old == key) {
-                atomicAdd(&L.u.t.vcnt[s], 1u);
+                if (distinct_first(L.u.t.dset, kFastDistinctBits, s, (uint32_t)tq, &L.overflow))
+                    atomicAdd(&L.u.t.vcnt[s], 1u);
                 atomicMin(&L.u.t.vmin[s], (uint32_t)tq);
                 atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
                 break;
@@ -992,10 +1033,10 @@ void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hi
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
-                  int parts, int stage, hipStream_t s) {
+                  int parts, int stage, uint32_t *dset, int dset_bits, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
-                   nrows, tomb_live, hot, parts, nullptr};
+                   nrows, tomb_live, hot, parts, nullptr, nullptr, dset, dset_bits};
     // stage = 0: all three kernels; 1, 2, 3: K5a, K5h, K5b alone (the engine times them one by one)
     if (stage == 0 || stage == 1) timed_launch(k_vote_hist, dim3(nq * parts), dim3(1024), 0, s, qp);
     if (stage == 0 || stage == 2)

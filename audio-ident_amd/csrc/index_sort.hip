@@ -1,5 +1,6 @@
 // index_sort.hip -- K4 index build as a key sort: a hand-written LSD radix sort for gfx950 (default),
-// rocPRIM's onesweep kept only as an A/B reference (aid_engine_force K4_BUILD).
+// rocPRIM's onesweep kept only as an A/B reference (aid_engine_force K4_BUILD 3), compiled only into the
+// diagnostic variant build -DAID_K4_ROCPRIM_AB (build_ext.build(variant="k4rocprim")), never into libaidfp.so.
 //
 // Replaces the LMDB put of `olaf_c store` (audio-ident-service/app/audio/fingerprint.py:117-125;
 // SURVEY.md 8a row a4). The index is a direct-address CSR over key26 = bucket_key(hash) (aidfp_layout.h, a bit
@@ -35,7 +36,9 @@
 // plus ~4 per distinct key (E) and the 2 KB of counts per tile per pass.
 #include <atomic>
 
+#ifdef AID_K4_ROCPRIM_AB  // diagnostic variant build only (build_ext.build(variant="k4rocprim")); never in libaidfp.so
 #include <rocprim/device/device_radix_sort.hpp>
+#endif
 
 #include "aidfp_device.h"
 
@@ -501,32 +504,44 @@ static void scan8(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, h
 }
 
 // ---- the device property ARANK relies on, checked once per device before the first build that would use it ----
-// Every wave of 64 workgroups adds 1 to one of its own 512 LDS counters per lane, 64 times, with digit patterns from
-// all-distinct to all-equal; for every pair of lanes l < l' that hit the same counter in one instruction, l' must get
-// the larger old value. *viol counts the pairs that do not (0 on gfx950: profiles/r05n_lds_atomic_order.json)
-__global__ __launch_bounds__(256) void k_lds_lane_order(uint32_t *__restrict__ viol) {
-    __shared__ uint32_t cnt[4][kDigits];
-    __shared__ uint32_t ret[4][64];
-    __shared__ uint32_t dig[4][64];
+// The probe issues the scatter's own pattern: every wave of three resident 256-thread workgroups per CU
+// adds 1 to its own 512 LDS counters kSlots times back to back (one item per lane per slot, no barrier between the
+// atomics), with digit patterns from all-distinct to all-equal mixed across the slots; then every item's old value
+// must equal the number of earlier items (slot by slot, lanes in lane order) of the wave with the same digit -- the
+// stable rank k_radix_scatter<ARANK> takes from it. *viol counts the items that do not (0 on gfx950:
+// profiles/r05n_lds_atomic_order.json for the one-atomic form of this probe)
+__global__ __launch_bounds__(kSortThreads, 3) void k_lds_lane_order(uint32_t *__restrict__ viol) {
+    __shared__ uint32_t cnt[kSortWaves][kDigits];
+    __shared__ uint16_t dig[kSortWaves][kSlots][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < 4 * kDigits; i += 256) (&cnt[0][0])[i] = 0u;
-    __syncthreads();
     uint32_t v = 0;
-    for (int r = 0; r < 64; ++r) {
-        uint32_t x = (blockIdx.x * 0x9E3779B9u) ^ (r * 0x85EBCA6Bu) ^ (w * 0xC2B2AE35u) ^ (lane * 0x27D4EB2Fu);
-        x ^= x >> 15;
-        x *= 0x2C1B3C6Du;
-        x ^= x >> 12;
-        const int p = r & 3;
-        const uint32_t d = p == 0 ? x & (kDigits - 1) : p == 1 ? x & 3u : p == 2 ? 5u : (x & 1u) ? (x >> 1) & 7u : 300u;
-        const uint32_t old = atomicAdd(&cnt[w][d], 1u);
-        ret[w][lane] = old;
-        dig[w][lane] = d;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int l2 = lane + 1; l2 < 64; ++l2) v += (dig[w][l2] == d && ret[w][l2] <= old) ? 1u : 0u;
-        __builtin_amdgcn_wave_barrier();
+    for (int r = 0; r < 4; ++r) {
+        for (int i = threadIdx.x; i < kSortWaves * kDigits; i += kSortThreads) (&cnt[0][0])[i] = 0u;
+        __syncthreads();
+        uint32_t d[kSlots], old[kSlots];
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            uint32_t x = (blockIdx.x * 0x9E3779B9u) ^ ((r * kSlots + s) * 0x85EBCA6Bu) ^ (w * 0xC2B2AE35u) ^
+                         (lane * 0x27D4EB2Fu);
+            x ^= x >> 15;
+            x *= 0x2C1B3C6Du;
+            x ^= x >> 12;
+            const int p = (s + r + (int)blockIdx.x) & 3;
+            d[s] = p == 0 ? x & (kDigits - 1) : p == 1 ? x & 3u : p == 2 ? 5u : (x & 1u) ? (x >> 1) & 7u : 300u;
+        }
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) old[s] = atomicAdd(&cnt[w][d[s]], 1u);  // back to back, as the scatter
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) dig[w][s][lane] = (uint16_t)d[s];
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+            uint32_t want = 0;
+            for (int s2 = 0; s2 <= s; ++s2)
+                for (int l2 = 0; l2 < (s2 < s ? 64 : lane); ++l2) want += dig[w][s2][l2] == d[s] ? 1u : 0u;
+            v += old[s] != want ? 1u : 0u;
+        }
+        __syncthreads();
     }
     if (v) atomicAdd(viol, v);
 }
@@ -539,7 +554,9 @@ static int lds_lane_order_ok(uint32_t *dev_word, hipStream_t s) {
     const int st = state[dev].load();
     if (st) return st == 1 ? 1 : 0;
     if (hipMemsetAsync(dev_word, 0, sizeof(uint32_t), s) != hipSuccess) return -1;
-    hipLaunchKernelGGL(k_lds_lane_order, dim3(64), dim3(256), 0, s, dev_word);
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    hipLaunchKernelGGL(k_lds_lane_order, dim3((unsigned)(3 * std::max(cus, 1))), dim3(kSortThreads), 0, s, dev_word);
     uint32_t viol = 1;
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(&viol, dev_word, sizeof(viol), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -549,7 +566,8 @@ static int lds_lane_order_ok(uint32_t *dev_word, hipStream_t s) {
     return viol == 0 ? 1 : 0;
 }
 
-// ---- rocPRIM reference build (A/B only) ----
+// ---- rocPRIM reference build (A/B only, in the AID_K4_ROCPRIM_AB variant build) ----
+#ifdef AID_K4_ROCPRIM_AB
 __global__ void k_sort_keys(const uint32_t *__restrict__ ph, const uint32_t *__restrict__ ptrack,
                             const uint32_t *__restrict__ pt, int64_t n, const uint8_t *__restrict__ tomb,
                             uint32_t n_tracks, uint32_t *__restrict__ keys, uint64_t *__restrict__ vals) {
@@ -559,6 +577,7 @@ __global__ void k_sort_keys(const uint32_t *__restrict__ ph, const uint32_t *__r
         vals[i] = (uint64_t)tr | ((uint64_t)pt[i] << 32);
     }
 }
+#endif
 
 void launch_make_sig(const uint64_t *post, int64_t n, uint16_t *sig, hipStream_t s);  // index.hip
 
@@ -574,11 +593,24 @@ size_t radix_scratch_u32(int64_t n) {
 
 // temporary storage of the rocPRIM sort for n pairs
 size_t index_sort_temp_bytes(int64_t n) {
+#ifdef AID_K4_ROCPRIM_AB
     size_t bytes = 0;
     rocprim::double_buffer<uint32_t> k(nullptr, nullptr);
     rocprim::double_buffer<uint64_t> v(nullptr, nullptr);
     if (rocprim::radix_sort_pairs(nullptr, bytes, k, v, (size_t)n, 0, kSortKeyBits) != hipSuccess) return 0;
     return bytes;
+#else
+    (void)n;
+    return 0;
+#endif
+}
+
+bool k4_ab_sort_built() {
+#ifdef AID_K4_ROCPRIM_AB
+    return true;
+#else
+    return false;
+#endif
 }
 
 // the three passes of the hand-written sort: SoA postings -> (keys1, vals1) -> (keys0, vals0) -> the CSR's values in
@@ -636,6 +668,9 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
     uint32_t *stmp = scratch + 2 * c;
     const uint32_t *sorted_keys = nullptr;
     if (n > 0 && use_rocprim) {
+#ifndef AID_K4_ROCPRIM_AB
+        return hipErrorNotSupported;
+#else
         const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_sort_keys, dim3((unsigned)blocks), dim3(256), 0, s, ph, ptrack, pt, n, tomb, n_tracks,
                            keys0, vals0);
@@ -646,6 +681,7 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
         if (err != hipSuccess) return err;
         sorted_keys = k.current();
         *vals_out = v.current();
+#endif
     } else if (n > 0) {
         uint32_t *counts = scratch, *offs = scratch + c;
         // rank_mode 0: the one-atomic rank where the device serves same-address LDS lanes in order, 1: ballots
@@ -663,11 +699,13 @@ hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, c
                                 tiles, s);
         *vals_out = vals1;
     }
+#ifdef AID_K4_ROCPRIM_AB
     if (n > 0 && sorted_keys) {  // rocPRIM: run ends from its sorted keys, the signatures from its values
         const int64_t blocks = std::min<int64_t>((n + 255) / 256, 16384);
         hipLaunchKernelGGL(k_run_ends, dim3((unsigned)blocks), dim3(256), 0, s, sorted_keys, n, E, nz);
         launch_make_sig(*vals_out, n, sig, s);
     }
+#endif
     // the hand-written sort wrote E in its last pass; its live keys are the nonzero E entries
     scan8<true>(E, offsets, K, stmp, s, sorted_keys ? nullptr : nz);
     return hipGetLastError();

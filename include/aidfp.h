@@ -64,7 +64,7 @@ typedef struct aid_config {
     int32_t hop;           /* 0 = FPSPEC default: 512 at sr >= 32 kHz, else 256 */
     float peak_threshold;  /* 0 = FPSPEC default 4.0; otherwise in [2^-124, 2^100] */
     int32_t device;        /* HIP device ordinal; -1 = current device */
-    int32_t min_match;     /* query: 0 = FPSPEC default 12 */
+    int32_t min_match;     /* query: 0 = FPSPEC default 10 (distinct query anchor frames, FPSPEC v1 7) */
     int32_t max_results;   /* query: 0 = FPSPEC default 50 */
     int32_t flags;         /* AID_FLAG_* (0 = default) */
     int32_t reserved[9];
@@ -98,7 +98,8 @@ int aid_engine_config(const aid_engine *e, aid_config *out);
 #define AID_FORCE_K5_PARTS 2       /* 0 by vote count, else 1, 2 or 4 key partitions per query (K5a) */
 #define AID_FORCE_K5_BATCH 3       /* 0 default (2048), else global-path queries per launch */
 #define AID_FORCE_K2_STRIPS_X100 4 /* 0 adaptive, else 100 x K2 strips per resident workgroup slot */
-#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B),
+#define AID_FORCE_K4_BUILD 5       /* 0 default, 1 radix sort (the default), 2 atomic counting sort, 3 rocPRIM sort (A/B; only in the
+                                      diagnostic variant library, else AID_ERR_INVALID),
                                       4 radix sort with the ballot-matched in-wave rank (A/B of the one-atomic rank) */
 #define AID_FORCE_EXCHANGE_FAIL 6  /* 1: the next index exchange's pack (aid_index_pack, or the prepare step of
                                       aid_index_allgather) fails with AID_ERR_NOMEM, once (rank-failure tests) */

@@ -1,5 +1,6 @@
 /*
- * fp_match.c -- CPU restatement of spec/FPSPEC.md section 7 (index + query).
+ * fp_match.c -- CPU restatement of spec/FPSPEC.md section 7 (index + query), FPSPEC v1: a (track, d)
+ * scores the distinct query anchor frames that vote for it (v0 counted the votes themselves).
  * TEST INFRASTRUCTURE ONLY (see fp_oracle.c header): it checks the GPU
  * index/match kernels; it is never the product path.
  *
@@ -72,11 +73,17 @@ int64_t fp_query(const fp_posting *p, int64_t np, const uint32_t *qhash, const u
         uint32_t tr = v[i].track;
         fp_row best = {0, tr, 0, 0, 0};
         while (i < nv && v[i].track == tr) {
-            int32_t d = v[i].d, cnt = 0, lo = v[i].tq, hi = v[i].tq;
+            /* FPSPEC v1 7: the score of (track, d) is the number of DISTINCT query anchor frames t_q among its
+               votes (votes are sorted by (track, d, t_q), so a new t_q is a change from the previous vote) */
+            int32_t d = v[i].d, cnt = 0, lo = v[i].tq, hi = v[i].tq, last = 0;
+            int first = 1;
             while (i < nv && v[i].track == tr && v[i].d == d) {
                 if (v[i].tq < lo) lo = v[i].tq;
                 if (v[i].tq > hi) hi = v[i].tq;
-                ++cnt; ++i;
+                if (first || v[i].tq != last) ++cnt;
+                last = v[i].tq;
+                first = 0;
+                ++i;
             }
             if (cnt > best.match_count) { best.match_count = cnt; best.d = d; best.tq_min = lo; best.tq_max = hi; }
         }

@@ -32,7 +32,7 @@ def test_abi_version_and_defaults_without_gpu():
     assert L.aid_abi_version() == 1
     cfg = _lib.AidConfig()
     assert L.aid_config_default(44100, ctypes.byref(cfg)) == 0
-    assert (cfg.hop, cfg.min_match, cfg.max_results) == (512, 12, 50)
+    assert (cfg.hop, cfg.min_match, cfg.max_results) == (512, 10, 50)  # FPSPEC v1 7
     assert abs(cfg.peak_threshold - 4.0) < 1e-9
     assert L.aid_config_default(16000, ctypes.byref(cfg)) == 0 and cfg.hop == 256
     assert L.aid_config_default(0, ctypes.byref(cfg)) == _lib.AID_ERR_INVALID
@@ -57,3 +57,18 @@ def test_resample_len_without_gpu():
     assert L.aid_resample_len(1000, 44100, 48000) == 1089  # ceil(1000 * 160 / 147)
     assert L.aid_resample_len(0, 48000, 16000) == 0
     assert L.aid_resample_len(10, 0, 16000) == 0
+
+
+def test_product_library_links_no_rocprim():
+    """rocPRIM's radix sort is the K4 A/B reference of the diagnostic variant build only; the product
+    library defines no symbol of it (its code would appear as rocprim:: template instances)."""
+    import shutil
+    import subprocess
+
+    import pytest
+
+    if not shutil.which("nm"):
+        pytest.skip("nm not available")
+    out = subprocess.run(["nm", "-C", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "rocprim::" not in out

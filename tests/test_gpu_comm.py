@@ -245,6 +245,6 @@ def test_world2_exchange_on_one_gpu():
         assert np.array_equal(union, expect)
         assert n_tracks == 13
         for rec, row in zip(recs, rows):
-            ref = O.query(union, rec, min_match=12, max_rows=50)
+            ref = O.query(union, rec, min_match=10, max_rows=50)  # the FPSPEC v1 default of the ranks' engines
             assert np.array_equal(row, ref)
         assert [int(x[0, 1]) if len(x) else None for x in rows] == [1, 11, 12, None]

@@ -125,6 +125,28 @@ def test_synth_generators_bit_identical(gpu_engine, sr, envelope, noise):
         assert np.array_equal(host[c], (ref.astype(np.float32) / np.float32(32768.0)).astype(np.float32)), c
 
 
+def test_synth_async_two_streams(gpu_engine):
+    """Two AID_SYNTH_ASYNC calls on different streams: the second call's uploads of its track and
+    start arrays must not overwrite the first call's while its kernel still reads them -- both outputs equal
+    the host generator."""
+    import torch
+
+    n = 44100 * 4
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    ta, sa = np.arange(40, 104, dtype=np.uint32), np.arange(64, dtype=np.int64) * 1000
+    tb, sb = np.arange(900, 964, dtype=np.uint32), np.arange(64, dtype=np.int64) * 777 + 5
+    a = torch.empty(64 * n, dtype=torch.float32, device="cuda")
+    b = torch.empty(64 * n, dtype=torch.float32, device="cuda")
+    gpu_engine.synth(a.data_ptr(), ta, sa, n, stream=s1.cuda_stream, wait=False)
+    gpu_engine.synth(b.data_ptr(), tb, sb, n, stream=s2.cuda_stream, wait=False)
+    s1.synchronize()
+    s2.synchronize()
+    ha, hb = a.cpu().numpy().reshape(64, n), b.cpu().numpy().reshape(64, n)
+    for c in (0, 31, 63):
+        assert np.array_equal(ha[c], synth.synth(int(ta[c]), int(sa[c]), n, SR)), c
+        assert np.array_equal(hb[c], synth.synth(int(tb[c]), int(sb[c]), n, SR)), c
+
+
 def test_logmag_tolerance(gpu_engine):
     """STFT magnitudes within 1e-4 rel (frame-normalised), log-mag within 60 dB of the peak."""
     x = _clip(3, 220500, snr=20)

@@ -244,9 +244,9 @@ def test_zero_hash_track_has_a_slot():
 
 
 def test_sort_build_equals_atomic_build():
-    """K4 hand-written radix-sort build (index_sort.hip, default) vs the atomic counting sort (force k4_build 2)
-    and rocPRIM's sort (3): same live
-    postings and identical query rows, with removed tracks (sentinel keys sorted past the live ones)."""
+    """K4 hand-written radix-sort build (index_sort.hip, default), its ballot-ranked form (force k4_build 4) and the
+    atomic counting sort (force 2): same live postings and identical query rows, with removed tracks (sentinel keys
+    sorted past the live ones)."""
     import torch
 
     n = SR * 12
@@ -255,10 +255,10 @@ def test_sort_build_equals_atomic_build():
     qs = [synth.synth(int(tracks[i]), int(rng.integers(0, 7 * SR)), 5 * SR, SR, snr_db=20.0, salt=40 + i)
           for i in range(0, 20, 2)]
     out = {}
-    for mode in ("atomic", "sort", "rocprim"):
+    for mode in ("atomic", "sort", "ballot"):
         eng = Engine(SR)
         try:
-            eng.force("k4_build", {"atomic": 2, "sort": 1, "rocprim": 3}[mode])
+            eng.force("k4_build", {"atomic": 2, "sort": 1, "ballot": 4}[mode])
             pcm = torch.empty(len(tracks) * n, dtype=torch.float32, device="cuda")
             eng.synth(pcm.data_ptr(), tracks, np.zeros(len(tracks), np.int64), n)
             eng.extract_device(pcm.data_ptr(), np.arange(len(tracks) + 1, dtype=np.int64) * n)
@@ -270,8 +270,8 @@ def test_sort_build_equals_atomic_build():
             out[mode] = (eng.index_stats(), eng.query(recs))
         finally:
             eng.close()
-    (sa, ra), (ss, rs), (sr, rr) = out["atomic"], out["sort"], out["rocprim"]
-    assert sr == ss and all(np.array_equal(a, b) for a, b in zip(rr, rs))  # hand-written sort == rocPRIM's
+    (sa, ra), (ss, rs), (sr, rr) = out["atomic"], out["sort"], out["ballot"]
+    assert sr == ss and all(np.array_equal(a, b) for a, b in zip(rr, rs))  # one-atomic rank == ballot rank
     assert sa["live"] == ss["live"] > 0 and sa["postings"] == ss["postings"]
     assert any(len(r) for r in rs)
     for q, (a, b) in enumerate(zip(ra, rs)):
@@ -283,7 +283,7 @@ def test_sort_build_equals_atomic_build():
 @pytest.mark.parametrize("removed", [False, True])
 def test_sort_build_many_column_groups(removed):
     """The radix build over more than one column-scan group (> 256 tiles of 4096 postings, ~1.4 M postings here), with
-    and without tombstones (the templated first pass): rows equal rocPRIM's build for 48 queries."""
+    and without tombstones (the templated first pass): rows equal the atomic counting build's for 48 queries."""
     import torch
 
     n = SR * 12
@@ -294,10 +294,10 @@ def test_sort_build_many_column_groups(removed):
           for i in pick]
     recs = [O.fingerprint(q, HOP) for q in qs]
     out = {}
-    for mode in ("sort", "rocprim"):
+    for mode in ("sort", "atomic"):
         eng = Engine(SR)
         try:
-            eng.force("k4_build", {"sort": 1, "rocprim": 3}[mode])
+            eng.force("k4_build", {"sort": 1, "atomic": 2}[mode])
             pcm = torch.empty(200 * n, dtype=torch.float32, device="cuda")
             for b0 in range(0, len(tracks), 200):
                 tr = tracks[b0:b0 + 200]
@@ -313,8 +313,8 @@ def test_sort_build_many_column_groups(removed):
             out[mode] = (st, eng.query(recs))
         finally:
             eng.close()
-    (ss, rs), (sr, rr) = out["sort"], out["rocprim"]
-    assert ss == sr
+    (ss, rs), (sr, rr) = out["sort"], out["atomic"]
+    assert ss["live"] == sr["live"] and ss["postings"] == sr["postings"]
     assert all(np.array_equal(a, b) for a, b in zip(rs, rr))
     hits = [int(r[0, 1]) if len(r) else None for r in rs]
     gone = {int(tracks[i]) for i in pick[:5]} if removed else set()
@@ -343,10 +343,10 @@ def _csr_mirror(post, removed):
     return offs, posts
 
 
-@pytest.mark.parametrize("mode", ["sort", "ballot", "rocprim"])
+@pytest.mark.parametrize("mode", ["sort", "ballot"])
 def test_csr_layout_equals_stable_mirror(mode):
     """The built CSR itself, not only the rows queries read from it: the hand-written radix build (its default rank,
-    one LDS atomic per posting; and the ballot-matched rank, force 4), and rocPRIM's, the A/B reference, lay out
+    one LDS atomic per posting; and the ballot-matched rank, force 4) lays out
     exactly the stable key sort of the stored postings (arrival order inside a bucket), with
     removed tracks' postings dropped and offsets equal to the key histogram's prefix sums; over more than one K4
     tile and column group (~1.4 M postings)."""
@@ -357,7 +357,7 @@ def test_csr_layout_equals_stable_mirror(mode):
     removed = {int(tracks[3]), int(tracks[300]), int(tracks[599])}
     eng = Engine(SR)
     try:
-        eng.force("k4_build", {"sort": 1, "ballot": 4, "rocprim": 3}[mode])
+        eng.force("k4_build", {"sort": 1, "ballot": 4}[mode])
         pcm = torch.empty(200 * n, dtype=torch.float32, device="cuda")
         for b0 in range(0, len(tracks), 200):
             tr = tracks[b0:b0 + 200]
@@ -377,6 +377,19 @@ def test_csr_layout_equals_stable_mirror(mode):
     bad = np.flatnonzero(posts != ref_posts)
     assert len(bad) == 0, f"{len(bad)} CSR postings out of place, first at {bad[:5]}"
     assert np.array_equal(offs, ref_offs)
+
+
+def test_rocprim_ab_not_in_product_library():
+    """The rocPRIM sort is an A/B reference of the diagnostic variant build only: the product
+    library refuses k4_build 3 and links no rocPRIM code."""
+    from aidfp._lib import EngineError
+
+    eng = Engine(SR)
+    try:
+        with pytest.raises(EngineError):
+            eng.force("k4_build", 3)
+    finally:
+        eng.close()
 
 
 def test_csr_export_needs_a_finalized_index():

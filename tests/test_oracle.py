@@ -128,6 +128,20 @@ def test_match_oracle_votes():
     assert sorted(r[1] for r in rows) == [7, 8]
 
 
+def test_match_oracle_counts_distinct_anchor_frames():
+    """FPSPEC v1 7: a (track, d) scores the DISTINCT query anchor frames among its votes. Query frame 0 holds two
+    records (hashes 11 and 14) that both vote (7, d = 100): 4 votes, 3 distinct frames -> match_count 3. Track 8
+    gets 3 votes for d = 40, all from frame 10 (one onset's harmonics): match_count 1, below min_match 2."""
+    post = np.array([[11, 7, 100], [14, 7, 100], [12, 7, 101], [13, 7, 102],
+                     [21, 8, 50], [22, 8, 50], [23, 8, 50]], dtype=np.uint32)
+    qh = np.array([11, 14, 12, 13, 21, 22, 23], dtype=np.uint64)
+    qt = np.array([0, 0, 1, 2, 10, 10, 10], dtype=np.uint64)
+    rows = O.query(post, qh | (qt << np.uint64(32)), min_match=1)
+    assert rows.tolist() == [[3, 7, 100, 0, 2], [1, 8, 40, 10, 10]]
+    rows = O.query(post, qh | (qt << np.uint64(32)), min_match=2)
+    assert rows.tolist() == [[3, 7, 100, 0, 2]]
+
+
 def test_numpy_scipy_path_matches_on_synthetic_clips():
     """The bench's NumPy/SciPy cpu_baseline leg (float64 FFT) gives the spec's records on the synthetic
     workloads (band-limited and full-band, clean and noisy): its timing is for the same output."""
