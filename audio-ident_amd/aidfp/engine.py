@@ -65,7 +65,7 @@ def on_shutdown(obj) -> None:
 
 
 def _shutdown() -> None:
-    global _shutdown_done
+    global _shutdown_done, _copy_pool
     if _shutdown_done:
         return
     for obj in list(_closers):
@@ -73,6 +73,27 @@ def _shutdown() -> None:
             obj.close()
         except Exception:  # teardown goes on: every engine must still be destroyed
             pass
+    # no thread of ours may still be inside a copy into a page-locked buffer or an engine call when the engines and
+    # the buffers go: the PCM copy pool is joined, then every engine's streams and the device drained (VERDICT r5
+    # next #2) before aid_engine_destroy (which also takes each engine's lock: a call still running finishes first)
+    pool, _copy_pool = _copy_pool, None
+    if pool is not None:
+        try:
+            pool.shutdown(wait=True)
+        except Exception:
+            pass
+    for e in list(_live):
+        try:
+            e.sync()
+        except Exception:
+            pass
+    try:
+        import torch
+
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
     for e in list(_live):
         try:
             e.close()

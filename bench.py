@@ -181,6 +181,55 @@ def parity(eng, host_pcm: np.ndarray, ref=None) -> dict:
             "mismatched_clips": bad[:8], "oracle": "oracle/fp_oracle.c"}
 
 
+MAG_BANDS_DB = ((0, 20), (20, 40), (40, 60), (60, 80))
+MAG_REL_TOL = 1e-4  # north_star: "STFT magnitudes match within 1e-4 rel"
+MAG_TOL_WITHIN_DB = 60  # ... per bin, for every bin within this many dB of its frame's peak
+
+
+def magnitude_parity(host_pcm: np.ndarray, clips: int = 4, sr: int = 44100) -> dict:
+    """Per-bin relative error of the product path's binary32 power (aid_result_power of an AID_FLAG_KEEP_POWER
+    engine, K1's own output) against float64 numpy (oracle.stft_power_f64: pocketfft of the same frames), as
+    magnitudes |sqrt(P) - sqrt(P64)| / sqrt(P64), bucketed by dB below the frame's peak.
+    binary32 delivers 1e-4 per bin down to MAG_TOL_WITHIN_DB below the frame peak (a bin's absolute rounding
+    error is set by the frame's energy, so its relative error grows as the bin falls below the peak);
+    `ok` asserts exactly that band. The power bits are also checked against the C oracle."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O  # checker only
+
+    from aidfp.engine import Engine
+
+    x = [np.ascontiguousarray(c) for c in host_pcm[:clips]]
+    hop = 512 if sr >= 32000 else 256  # FPSPEC 1
+    stats = {f"{a}-{b}dB": {"bins": 0, "max_rel": 0.0} for a, b in MAG_BANDS_DB}
+    p999 = {k: [] for k in stats}
+    bits_equal = True
+    with Engine(sr, keep_power=True) as eng:
+        eng.extract_host(x)
+        for c, xc in enumerate(x):
+            P = eng.power(c, len(xc))
+            bits_equal &= bool(np.array_equal(P.view(np.uint32), O.stft_power(xc, hop).view(np.uint32)))
+            R = O.stft_power_f64(xc, hop)
+            peak = R.max(axis=1, keepdims=True)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                db = 10.0 * np.log10(peak / R)
+                rel = np.abs(np.sqrt(P.astype(np.float64)) - np.sqrt(R)) / np.sqrt(R)
+            for (a, b), k in zip(MAG_BANDS_DB, stats):
+                m = (db >= a) & (db < b) & (R > 0)
+                if m.any():
+                    stats[k]["bins"] += int(m.sum())
+                    stats[k]["max_rel"] = max(stats[k]["max_rel"], float(rel[m].max()))
+                    p999[k].append(float(np.percentile(rel[m], 99.9)))
+    for k in stats:
+        stats[k]["p999_rel"] = max(p999[k]) if p999[k] else None
+        stats[k]["max_rel"] = float(f"{stats[k]['max_rel']:.3e}")
+    within = [k for (a, b), k in zip(MAG_BANDS_DB, stats) if b <= MAG_TOL_WITHIN_DB]
+    return {"clips": len(x), "per_bin": stats, "tolerance_rel": MAG_REL_TOL, "tolerance_within_db": MAG_TOL_WITHIN_DB,
+            "ok": bits_equal and all(stats[k]["max_rel"] <= MAG_REL_TOL for k in within),
+            "power_bits_equal_oracle": bits_equal,
+            "note": "magnitude = sqrt(binary32 power of K1) vs sqrt(float64 numpy power), per bin; bands in dB below "
+                    "the frame's peak power"}
+
+
 def cpu_baseline(host_pcm: np.ndarray, min_s: float = 6.0) -> tuple[dict, list]:
     """The C oracle on the host cores over the bench batch: passes of all 256 clips on every usable core until
     `min_s` seconds have elapsed (>= 1 pass), then 64 clips on one thread; then the NumPy/SciPy path
@@ -1179,6 +1228,11 @@ def main() -> int:
             ref, cpu = cpu_baseline(host)
         # untimed: the batch's hashes (from the last step) against the oracle's
         par = parity(eng, host, ref)
+        if world == 1:  # per-bin magnitude criterion (north_star 1e-4 rel) on 4 clips of the batch, untimed
+            try:
+                par["magnitude"] = magnitude_parity(host, 4, SR)
+            except Exception as exc:  # reported, never fatal: the hashes above are the gate
+                par["magnitude"] = {"ok": False, "error": f"{type(exc).__name__}: {exc}"}
 
     _log("headline done; cpu baseline / parity done")
     fullband = None

@@ -111,3 +111,40 @@ def test_resample_batch_equals_single_streams(gpu_engine):
             torch.cuda.synchronize()
             assert torch.equal(out_b[i, :cnt], one), (sr_in, sr_out, ch, i)
             assert not out_b[i, cnt:].any()
+
+
+def test_stream_bank_equals_oracle_route():
+    """The production streaming path: StreamBank with 6 live 48 kHz stereo streams in lockstep
+    against a 16 kHz index ingested from 44.1 kHz sources (the reference's deployment shape), pushed in 1.37 s
+    chunks so windows straddle chunk boundaries; the first 4 streams' windows equal the oracle route -- host
+    downmix, oracle/fp_resample.c 48k -> 16k, oracle/fp_oracle.c per window, oracle/fp_match.c over this index's
+    postings (bench.stream_parity, the check the bench's stream key runs)."""
+    import bench
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.stream import StreamBank
+
+    SSR, QSR = 16000, 48000
+    with Engine(SSR) as eng:
+        ingest_synthetic(eng, np.arange(60, dtype=np.uint32), 30.0, batch=64, source_sr=44100, local=True)
+        eng.index_finalize()
+        S, n_seg, seg = 6, 2, 12 * QSR
+        seg_tracks = np.random.default_rng(3).integers(0, 60, (S, n_seg)).astype(np.uint32)
+        stereo = torch.empty(S, n_seg * seg, 2, dtype=torch.float32, device="cuda")
+        tmp = torch.empty(S * n_seg * seg, dtype=torch.float32, device="cuda")
+        for ch in range(2):
+            eng.synth(tmp.data_ptr(), seg_tracks.ravel(), np.zeros(S * n_seg, np.int64), seg,
+                      noise_a=synth.noise_halfwidth(30.0), salt=11 + ch, sample_rate=QSR)
+            stereo[:, :, ch] = tmp.view(S, n_seg * seg)
+        torch.cuda.synchronize()
+        bank = StreamBank(eng, S, stream_sr=QSR)
+        res = [[] for _ in range(S)]
+        chunk = int(1.37 * QSR)
+        for a in range(0, stereo.shape[1], chunk):
+            r = bank.push(stereo[:, a:a + chunk])
+            for i in range(S):
+                res[i] += r[i]
+        assert all(len(res[i]) == int((n_seg * 12.0 - 5.0) // 2.5) + 1 for i in range(S))
+        assert sum(len(w.rows) > 0 for i in range(S) for w in res[i]) > 0
+        par = bench.stream_parity(eng, stereo, seg_tracks, res, 4, torch, max_windows=8)
+    assert par["windows"] == 4 * 8
+    assert par["bit_exact"], par
