@@ -66,7 +66,7 @@ void launch_records_to_postings(const uint64_t *recs, const int64_t *src_off, co
 void launch_append_offsets(const int64_t *counts, int n_clips, int64_t base, int64_t *dst_off, int64_t *total,
                            hipStream_t s);
 void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
-                        const uint32_t *offsets, int64_t *votes, hipStream_t s);
+                        const uint32_t *offsets, int64_t *votes, uint64_t *ranges, hipStream_t s);
 void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq, const uint32_t *offsets,
                   const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks, int min_match, int max_rows,
                   uint32_t *hist, int hist_bits, uint32_t *hot, int32_t *rows, int32_t *nrows, int tomb_live,
@@ -77,7 +77,7 @@ void launch_index_checksum(const uint32_t *ph, const uint32_t *ptr, const uint32
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
                       int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, const int64_t *votes,
-                      const uint16_t *sig, hipStream_t s);
+                      const uint16_t *sig, const uint64_t *ranges, hipStream_t s);
 uint32_t index_keys();
 void launch_downmix(const float *in, int64_t n, float *out, hipStream_t s);
 void launch_window_gather(const float *src, const int64_t *win, int n_win, int64_t max_len, float *dst, hipStream_t s);
@@ -207,6 +207,7 @@ struct aid_engine {
     DevBuf<int32_t> q_rows, q_nrows;
     DevBuf<uint32_t> q_hot;  // K5h hot-bucket bitmaps, [batch][2^bits / 32]
     DevBuf<uint32_t> q_dset;  // K5b retries: HBM distinct (slot, t_q) sets, [batch][2^dbits]
+    DevBuf<uint64_t> q_ranges;  // K5: per query record its CSR range (k_query_votes -> k_match_lds)
     DevBuf<int64_t> q_votes;  // exact votes per query (LDS-histogram eligibility)
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
@@ -483,6 +484,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->q_hist.release();
     e->q_hot.release();
     e->q_dset.release();
+    e->q_ranges.release();
     e->q_rows.release();
     e->q_nrows.release();
     e->x_src.release();
@@ -2042,12 +2044,13 @@ int aid_index_load(aid_engine *e, const char *path) {
 constexpr double kForwardedPerBucket = 2.0;  // forwarded votes (1-bit filter estimate) per global histogram bucket
 // run K5 over nq queries whose records are at device ranges (q_start/q_count device arrays).
 // Exact per-query vote counts (k_query_votes) choose the path and size the vote histogram;
-// queries whose exact LDS table overflowed are re-run with 4x the buckets. (max_recs is unused.)
+// queries whose exact LDS table overflowed are re-run with 4x the buckets. rec_cap: elements of `recs` (the per-record
+// CSR range cache the vote count writes for the LDS path has one entry per record index).
 // rows == nullptr: device mode, every query's rows end in e->q_rows ([nq][max_results][5] int32);
 // nrows (host) is always filled
 
 static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstart_dev, const int64_t *qcount_dev,
-                       int nq, int64_t max_recs, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
+                       int nq, int64_t rec_cap, aid_match_row *rows, int32_t *nrows, hipStream_t s) {
     const int mr = e->cfg.max_results;
     HIP_TRY(e->q_rows.reserve((size_t)std::max(nq, 1) * mr * 5));
     HIP_TRY(e->q_nrows.reserve((size_t)std::max(nq, 1)));
@@ -2058,7 +2061,10 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     HIP_TRY(hipMemcpyAsync(h_count.data(), qcount_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     {  // exact vote counts: path choice and the global histogram's size
         HIP_TRY(e->q_votes.reserve((size_t)nq));
-        launch_query_votes(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->q_votes.p, s);
+        const bool ranges = e->k5_path == 0 || e->k5_path == 1;  // the LDS path reads them
+        if (ranges) HIP_TRY(e->q_ranges.reserve((size_t)std::max<int64_t>(rec_cap, 1)));
+        launch_query_votes(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->q_votes.p, ranges ? e->q_ranges.p : nullptr,
+                           s);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(h_votes.data(), e->q_votes.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     }
@@ -2075,7 +2081,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
-                             e->idx_sig.p, s);
+                             e->idx_sig.p, e->q_ranges.p, s);
         }
         HIP_TRY(hipGetLastError());
         spec_n.resize(nq);
@@ -2136,7 +2142,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
             ProfScope ps(e, AID_K_MATCH, s, true);
             launch_match_lds(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
                              e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
-                             e->idx_sig.p, s);
+                             e->idx_sig.p, e->q_ranges.p, s);
         }
         HIP_TRY(hipGetLastError());
         std::vector<int32_t> got_n(nq);
@@ -2276,7 +2282,8 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
     HIP_TRY(hipMemcpyAsync(e->q_count.p, ct.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
     int64_t mx = 0;
     for (int q = 0; q < nq; ++q) mx = std::max(mx, ct[q]);
-    return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, mx, rows, nrows, s);
+    (void)mx;
+    return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, std::max<int64_t>(n, 1), rows, nrows, s);
 }
 
 static int query_extracted_locked(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
@@ -2288,7 +2295,7 @@ static int query_extracted_locked(aid_engine *e, aid_match_row *rows, int32_t *n
     if (!rows || !nrows) return fail(AID_ERR_INVALID, "null output");
     HIP_TRY(e->q_start.reserve(nq));
     HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, -1, rows, nrows, s);
+    return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, (int64_t)e->records.n, rows, nrows, s);
 }
 
 int aid_query_extracted(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
@@ -2453,7 +2460,8 @@ static int exact_lane_locked(aid_engine *e, const float *pcm, const int64_t *off
         if (int rc = check_query_frames(e)) return rc;
         HIP_TRY(e->q_start.reserve(n_win));
         HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), n_win * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        if (int rc = run_queries(e, e->records.p, e->q_start.p, e->counts.p, n_win, -1, nullptr, nrows.data(), s))
+        if (int rc = run_queries(e, e->records.p, e->q_start.p, e->counts.p, n_win, (int64_t)e->records.n, nullptr,
+                                 nrows.data(), s))
             return rc;
         HIP_TRY(e->q_nrows.reserve((size_t)n_win));
         HIP_TRY(hipMemcpyAsync(e->q_nrows.p, nrows.data(), n_win * sizeof(int32_t), hipMemcpyHostToDevice, s));

@@ -275,6 +275,8 @@ struct QueryParams {
     int32_t parts;             // K5a workgroups (key partitions) per query
     const int64_t *votes;      // [nq] exact votes per query (k_query_votes, earlier on the stream); LDS path only
     const uint16_t *sig;       // [n] 2-B vote signature per posting (aidfp_layout.h posting_sig); LDS path only
+    const uint64_t *ranges;    // LDS path: per record (same index as recs) its CSR range p0 | p1 << 32, written by
+                               // k_query_votes earlier on the stream (nullptr: read offsets[] instead)
     uint32_t *dset;            // K5b: [nq][2^dset_bits] distinct (slot, t_q) sets in HBM, all kDistinctEmpty on entry
                                // (a retry of queries whose LDS set overflowed); nullptr = the LDS set
     int32_t dset_bits;
@@ -656,10 +658,16 @@ __device__ __forceinline__ ChunkGroup load_group(const QueryParams &qp, int64_t 
     uint32_t clen = 0;
     if (lane < chunk && i < n) {
         const uint64_t r = qp.recs[a + i];
-        const uint32_t k = key26((uint32_t)r);
         gr.tq = (int32_t)(r >> 32);
-        gr.p0 = qp.offsets[k];
-        gr.p1 = qp.offsets[k + 1];
+        if (qp.ranges) {  // coalesced, and independent of the record load (no recs -> offsets chain)
+            const uint64_t rg = qp.ranges[a + i];
+            gr.p0 = (uint32_t)rg;
+            gr.p1 = (uint32_t)(rg >> 32);
+        } else {
+            const uint32_t k = key26((uint32_t)r);
+            gr.p0 = qp.offsets[k];
+            gr.p1 = qp.offsets[k + 1];
+        }
         clen = gr.p1 > gr.p0 ? (gr.p1 + (kSigChunk - 1)) / kSigChunk - gr.p0 / kSigChunk : 0u;
     }
     uint32_t incl = clen;
@@ -996,10 +1004,10 @@ void k_match_lds(QueryParams qp) {
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
                       const uint32_t *offsets, const uint64_t *post, const uint8_t *tomb, uint32_t n_tracks,
                       int min_match, int max_rows, int32_t *rows, int32_t *nrows, int tomb_live, const int64_t *votes,
-                      const uint16_t *sig, hipStream_t s) {
+                      const uint16_t *sig, const uint64_t *ranges, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
-                   tomb_live, nullptr, 1, votes, sig};
+                   tomb_live, nullptr, 1, votes, sig, ranges};
     timed_launch(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
 }
 
@@ -1036,7 +1044,7 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
                   int parts, int stage, uint32_t *dset, int dset_bits, hipStream_t s) {
     if (nq <= 0) return;
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, hist, hist_bits, rows,
-                   nrows, tomb_live, hot, parts, nullptr, nullptr, dset, dset_bits};
+                   nrows, tomb_live, hot, parts, nullptr, nullptr, nullptr, dset, dset_bits};
     // stage = 0: all three kernels; 1, 2, 3: K5a, K5h, K5b alone (the engine times them one by one)
     if (stage == 0 || stage == 1) timed_launch(k_vote_hist, dim3(nq * parts), dim3(1024), 0, s, qp);
     if (stage == 0 || stage == 2)
@@ -1045,16 +1053,22 @@ void launch_query(const uint64_t *recs, const int64_t *qstart, const int64_t *qc
 }
 
 // exact vote count of each query: the sum of its records' bucket lengths (one block per query)
+// and (ranges != nullptr) every record's CSR range p0 | p1 << 32 at its record index, so the LDS match path reads the
+// ranges coalesced in both of its passes instead of two dependent random offset loads per record and pass (config 4's
+// ~650-record windows take more than one record group per wave, so the groups are loaded once per pass)
 __global__ __launch_bounds__(256) void k_query_votes(const uint64_t *__restrict__ recs, const int64_t *__restrict__ qstart,
                                                      const int64_t *__restrict__ qcount,
-                                                     const uint32_t *__restrict__ offsets, int64_t *__restrict__ votes) {
+                                                     const uint32_t *__restrict__ offsets, int64_t *__restrict__ votes,
+                                                     uint64_t *__restrict__ ranges) {
     __shared__ unsigned long long part[4];
     const int q = blockIdx.x;
     const int64_t a = qstart[q], n = qcount[q];
     unsigned long long v = 0;
     for (int64_t i = threadIdx.x; i < n; i += 256) {
         const uint32_t k = key26((uint32_t)recs[a + i]);
-        v += offsets[k + 1] - offsets[k];
+        const uint32_t p0 = offsets[k], p1 = offsets[k + 1];
+        v += p1 - p0;
+        if (ranges) ranges[a + i] = (uint64_t)p0 | ((uint64_t)p1 << 32);
     }
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
@@ -1063,8 +1077,9 @@ __global__ __launch_bounds__(256) void k_query_votes(const uint64_t *__restrict_
 }
 
 void launch_query_votes(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
-                        const uint32_t *offsets, int64_t *votes, hipStream_t s) {
-    if (nq > 0) hipLaunchKernelGGL(k_query_votes, dim3(nq), dim3(256), 0, s, recs, qstart, qcount, offsets, votes);
+                        const uint32_t *offsets, int64_t *votes, uint64_t *ranges, hipStream_t s) {
+    if (nq > 0)
+        hipLaunchKernelGGL(k_query_votes, dim3(nq), dim3(256), 0, s, recs, qstart, qcount, offsets, votes, ranges);
 }
 
 // number of non-empty buckets (for the query histogram sizing)
