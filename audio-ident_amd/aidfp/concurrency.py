@@ -127,16 +127,20 @@ class QueryCoalescer:
     than the cap runs alone), so many long uploads never land in one engine call."""
 
     def __init__(self, run_batch: Callable[[Sequence], Sequence], window_s: float = 0.0005, max_batch: int = 256,
-                 max_batch_bytes: int = 64 << 20):
+                 max_batch_bytes: int = 64 << 20, workers: int = 1):
         self._run = run_batch
         self.window_s = float(window_s)
         self.max_batch = int(max_batch)
         self.max_batch_bytes = int(max_batch_bytes)
-        self._held = None  # the request that did not fit the previous batch
+        # dispatcher threads: with two, one batch's host work (collection, the PCM copy into page-locked memory, row
+        # parsing, resolution) runs while the other batch is inside its engine call (which releases the GIL); the
+        # engine itself still runs one call at a time
+        self.workers = max(1, int(workers))
         self._last_batch = 0  # size of the previous batch: the collection window opens only after a batch > 1
         self._q: queue.SimpleQueue = queue.SimpleQueue()
-        self._thread: threading.Thread | None = None
+        self._threads: list[threading.Thread] = []
         self._start_lock = threading.Lock()
+        self._batches_lock = threading.Lock()
         self.batches: list[int] = []  # sizes of the last batches run (bounded; tests and stats)
 
     def submit(self, payload) -> Future:
@@ -158,23 +162,27 @@ class QueryCoalescer:
 
     def close(self) -> None:
         with self._start_lock:
-            t, self._thread = self._thread, None
-        if t is not None:
+            ts, self._threads = self._threads, []
+        for _ in ts:
             self._q.put(_STOP)
+        for t in ts:
             t.join()
 
     def _ensure_thread(self) -> None:
-        if self._thread is not None:
+        if self._threads:
             return
         with self._start_lock:
-            if self._thread is None:
-                t = threading.Thread(target=self._loop, name="aidfp-query-coalescer", daemon=True)
-                t.start()
-                self._thread = t
+            if not self._threads:
+                ts = [threading.Thread(target=self._loop, name=f"aidfp-query-coalescer-{i}", daemon=True)
+                      for i in range(self.workers)]
+                for t in ts:
+                    t.start()
+                self._threads = ts
 
     def _loop(self) -> None:
+        held = None  # the request that did not fit this thread's previous batch
         while True:
-            first, self._held = (self._held, None) if self._held is not None else (self._q.get(), None)
+            first, held = (held, None) if held is not None else (self._q.get(), None)
             if first is _STOP:
                 return
             batch = [first]
@@ -198,21 +206,21 @@ class QueryCoalescer:
                     stop = True
                     break
                 if nbytes + _size(item[0]) > self.max_batch_bytes:
-                    self._held = item  # opens the next batch
+                    held = item  # opens the next batch
                     break
                 nbytes += _size(item[0])
                 batch.append(item)
             self._dispatch(batch)
             if stop:
-                if self._held is not None:
-                    self._dispatch([self._held])
-                    self._held = None
+                if held is not None:
+                    self._dispatch([held])
                 return
 
     def _dispatch(self, batch) -> None:
         self._last_batch = len(batch)
-        self.batches.append(len(batch))
-        del self.batches[:-1024]
+        with self._batches_lock:
+            self.batches.append(len(batch))
+            del self.batches[:-1024]
         live = [(p, f) for p, f in batch if f.set_running_or_notify_cancel()]
         if not live:
             return

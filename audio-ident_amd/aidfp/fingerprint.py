@@ -106,14 +106,16 @@ class FingerprintService:
     write-ahead journal, so a store or delete writes O(track) bytes, not the whole index)."""
 
     def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20,
-                 coalesce_window_s: float = 0.0005, max_batch: int = 256, max_batch_bytes: int = 64 << 20):
+                 coalesce_window_s: float = 0.0005, max_batch: int = 256, max_batch_bytes: int = 64 << 20,
+                 coalesce_workers: int = 1):
         self.db_dir = Path(db_dir) if db_dir is not None else db_path()
         self.device = device
         self._rw = RWLock()  # index writers exclusive, queries shared
         self._init_lock = threading.Lock()  # first-use engine creation + index load
         # a coalesced batch holds at most max_batch requests and max_batch_bytes of PCM (64 MiB = 17 min of
         # 16 kHz audio): many long uploads cannot land in one extraction
-        self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch, max_batch_bytes)
+        self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch, max_batch_bytes,
+                                         coalesce_workers)
         self._ckpt_retry_at = 0.0  # monotonic time before which a failed auto-checkpoint is not retried
         self._engine = None
         self._store = None

@@ -962,7 +962,8 @@ def service_leg(args, rank, world, dist, torch) -> dict:
     levels = (1, 16, 64)
     out: dict = {}
     with tempfile.TemporaryDirectory() as db:
-        svc = fp.FingerprintService(Path(db), device=torch.cuda.current_device())
+        svc = fp.FingerprintService(Path(db), device=torch.cuda.current_device(),
+                                    coalesce_workers=args.service_workers)
         svc.persist = False
 
         def build():
@@ -1081,6 +1082,7 @@ def main() -> int:
                     help="streams whose first windows rank 0 checks against the oracle route (0 = none)")
     ap.add_argument("--no-service", action="store_true", help="skip the drop-in service leg")
     ap.add_argument("--service-tracks", type=int, default=10000)
+    ap.add_argument("--service-workers", type=int, default=1, help="coalescer dispatcher threads of the service leg")
     ap.add_argument("--service-requests", type=int, default=512)
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print one line per rank and exit without touching the GPU (tests)")
