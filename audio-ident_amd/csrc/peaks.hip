@@ -64,7 +64,12 @@ __device__ __forceinline__ int pkey(float x) {
 }
 
 // occupancy 4 forced by the launch bounds (<= 128 VGPRs, no spills)
-__global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ power, const ClipDesc *__restrict__ clips,
+#if defined(AID_K2_PF2) && defined(AID_K2_OCC3)
+__global__ __launch_bounds__(256, 3) void k_peak_pick(
+#else
+__global__ __launch_bounds__(256, 4) void k_peak_pick(
+#endif
+                                                  const float *__restrict__ power, const ClipDesc *__restrict__ clips,
                                                   int n_clips, int64_t f0, int64_t total_strips, int strip_len, float thr,
                                                   const uint64_t *__restrict__ hot, uint64_t *__restrict__ mask,
                                                   uint32_t *__restrict__ cold_cnt) {
@@ -198,6 +203,22 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rows_rsrc, off, 0, 0);
         return make_float4(__int_as_float(v[0]), __int_as_float(v[1]), __int_as_float(v[2]), __int_as_float(v[3]));
     };
+#if defined(AID_K2_PF2)
+    // diagnostic variant (timing A/B only, tools/variant_build.py ... -DAID_K2_PF2): rows fetched TWO steps ahead (8 rows
+    // in flight per thread) from two register buffers that alternate with the 8-row unroll (buffer s / 4)
+    float4 pfb[2][kRowsPerStep];
+    uint64_t hs[2][kRowsPerStep], hcur[kRowsPerStep];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < kRowsPerStep; ++j) {
+            const int r = rbeg + b * kRowsPerStep + j;
+            hs[b][j] = hotword(r);
+            pfb[b][j] = load_row(r, b * kRowsPerStep + j < iters ? hs[b][j] : 0ull);
+            hcur[j] = 0ull;
+        }
+    uint64_t hwv = hotwords(rbeg + 2 * kRowsPerStep);  // hot words of the rows the next staging fetches (lane & 3)
+#else
     float4 pf[kRowsPerStep];  // rows of the next step, in flight
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) pf[j] = load_row(rbeg + j, j < iters ? hotword(rbeg + j) : 0ull);
@@ -206,6 +227,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
     uint64_t hsave[kRowsPerStep], hcur[kRowsPerStep];
 #pragma unroll
     for (int j = 0; j < kRowsPerStep; ++j) hsave[j] = hcur[j] = hotword(rbeg + j);
+#endif
 
     for (int base = 0; base < iters; base += 8) {
 #pragma unroll
@@ -223,6 +245,21 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
 #endif
                 // stage rows it .. it+3 as keys, then fetch rows it+PF .. (register staging beats
                 // LDS-DMA here: 0.299 vs 0.323 ms at the same occupancy)
+#if defined(AID_K2_PF2)
+                const int b = (s / kRowsPerStep) & 1;  // compile-time after the 8-row unroll
+#pragma unroll
+                for (int j = 0; j < kRowsPerStep; ++j) {
+                    const float4 v = pfb[b][j];
+                    const int4 kv = make_int4(pkey(v.x), pkey(v.y), pkey(v.z), pkey(v.w));
+                    reinterpret_cast<int4 *>(&rows[j][16])[tid] = kv;
+                    bms[j][4 + tid] = max(max(kv.x, kv.y), max(kv.z, kv.w));
+                    const int rn = rbeg + it + j + 2 * kRowsPerStep;
+                    hcur[j] = hs[b][j];
+                    hs[b][j] = word_of(hwv, j);
+                    pfb[b][j] = load_row(rn, it + j + 2 * kRowsPerStep < iters ? hs[b][j] : 0ull);
+                }
+                hwv = hotwords(rbeg + it + 3 * kRowsPerStep);
+#else
 #pragma unroll
                 for (int j = 0; j < kRowsPerStep; ++j) {
                     const int slot = (s + j) % kRowsPerStep;  // compile-time: the loop is unrolled by 8
@@ -236,6 +273,7 @@ __global__ __launch_bounds__(256, 4) void k_peak_pick(const float *__restrict__ 
                     pf[slot] = load_row(rn, it + j + kRowsPerStep < iters ? hsave[j] : 0ull);
                 }
                 hwv = hotwords(rbeg + it + 2 * kRowsPerStep);
+#endif
                 __syncthreads();
             }
             const int r = rbeg + it;

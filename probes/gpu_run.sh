@@ -8,6 +8,8 @@
 #   k5req  the lane's memory-side read requests by size (TCC_EA0_RDREQ, TCC_EA0_RDREQ_32B) and TCP->TCC reads
 #   segv   VERDICT r5 #2: the r05y2 command (service leg under --kernel-trace --memory-copy-trace), once
 #   counters  rocprofv3 -L
+#   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/k2pf2 (probes/run_ab_lib.sh, 3 rounds)
+#   svcab  the service leg with 1 vs 2 coalescer dispatcher threads, interleaved, 2 rounds
 # Every step has its own time limit; the first failing step ends the run (exit 10 + step number).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -40,6 +42,13 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCP_TCC_READ_REQ_sum -T -d $O/k5/req -o run --output-format csv -- $B > $O/k5_req.json 2> $O/k5_req.err ;;
     segv) timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/segv.json 2> $O/segv.err ;;
     counters) timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 ;;
+    k2ab) timeout -k 10 900 bash probes/run_ab_lib.sh $O/k2pf2_ab.txt k2pf2 3 > $O/k2ab.log 2>&1 ;;
+    svcab)
+      rc=0
+      for r in 1 2; do for w in 1 2; do
+        timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-workers $w > $O/svc_w${w}_r$r.json 2> $O/svc_w${w}_r$r.err || { rc=$?; break 2; }
+      done; done
+      [ $rc -eq 0 ] ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
