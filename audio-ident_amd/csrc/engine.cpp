@@ -138,6 +138,29 @@ struct DevBuf {
     }
 };
 
+// page-locked host buffer (hipHostMalloc): device-to-host copies into it are asynchronous, so a call can queue its
+// result copies behind its kernels and wait once
+template <typename T>
+struct HostBuf {
+    T *p = nullptr;
+    size_t n = 0;  // capacity in elements
+    hipError_t reserve(size_t want) {  // callers have synchronised any copy still targeting the old buffer
+        if (want <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        const size_t cap = std::max(want, (size_t)64);
+        hipError_t e = hipHostMalloc((void **)&p, cap * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = cap;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 struct ProfEvent {
     int kernel;
     hipEvent_t a, b;
@@ -208,6 +231,9 @@ struct aid_engine {
     DevBuf<uint32_t> q_hot;  // K5h hot-bucket bitmaps, [batch][2^bits / 32]
     DevBuf<uint32_t> q_dset;  // K5b retries: HBM distinct (slot, t_q) sets, [batch][2^dbits]
     DevBuf<uint64_t> q_ranges;  // K5: per query record its CSR range (k_query_votes -> k_match_lds)
+    HostBuf<int64_t> hq_meta;   // run_queries: per query start, record count, exact votes (pinned: async D2H)
+    HostBuf<int32_t> hq_n;      // run_queries: the LDS path's per-query row counts
+    HostBuf<int32_t> hq_rows;   // run_queries: the LDS path's rows, [nq][max_results][5]
     DevBuf<int64_t> q_votes;  // exact votes per query (LDS-histogram eligibility)
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
@@ -485,6 +511,9 @@ void aid_engine_destroy(aid_engine *e) {
     e->q_hot.release();
     e->q_dset.release();
     e->q_ranges.release();
+    e->hq_meta.release();
+    e->hq_n.release();
+    e->hq_rows.release();
     e->q_rows.release();
     e->q_nrows.release();
     e->x_src.release();
@@ -2057,8 +2086,13 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     std::vector<int> todo(nq);
     for (int q = 0; q < nq; ++q) todo[q] = q;
     std::vector<int64_t> h_start(nq), h_count(nq), h_votes(nq, 0);
-    HIP_TRY(hipMemcpyAsync(h_start.data(), qstart_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h_count.data(), qcount_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    // the per-query metadata and (below) the LDS path's rows come back through page-locked buffers: the copies are
+    // queued behind the kernels and the call waits ONCE (a pageable destination made each copy a host wait, so K5
+    // was launched only after a round trip behind the extraction)
+    HIP_TRY(e->hq_meta.reserve((size_t)3 * nq));
+    int64_t *p_start = e->hq_meta.p, *p_count = p_start + nq, *p_votes = p_count + nq;
+    HIP_TRY(hipMemcpyAsync(p_start, qstart_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(p_count, qcount_dev, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     {  // exact vote counts: path choice and the global histogram's size
         HIP_TRY(e->q_votes.reserve((size_t)nq));
         const bool ranges = e->k5_path == 0 || e->k5_path == 1;  // the LDS path reads them
@@ -2066,7 +2100,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         launch_query_votes(recs, qstart_dev, qcount_dev, nq, e->idx_off.p, e->q_votes.p, ranges ? e->q_ranges.p : nullptr,
                            s);
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(h_votes.data(), e->q_votes.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(p_votes, e->q_votes.p, nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     }
     // the LDS path is launched right away, in the same round trip as the vote counts instead of after them (one
     // host sync less per call). It routes each query by its own count (K5 reads q_votes on the device): a query
@@ -2085,12 +2119,21 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         }
         HIP_TRY(hipGetLastError());
         spec_n.resize(nq);
-        if (rows)
-            HIP_TRY(hipMemcpyAsync(rows, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(spec_n.data(), e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        if (rows) {
+            HIP_TRY(e->hq_rows.reserve((size_t)nq * mr * 5));
+            HIP_TRY(hipMemcpyAsync(e->hq_rows.p, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row),
+                                   hipMemcpyDeviceToHost, s));
+        }
+        HIP_TRY(e->hq_n.reserve((size_t)nq));
+        HIP_TRY(hipMemcpyAsync(e->hq_n.p, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     }
     HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(h_start.data(), p_start, nq * sizeof(int64_t));
+    std::memcpy(h_count.data(), p_count, nq * sizeof(int64_t));
+    std::memcpy(h_votes.data(), p_votes, nq * sizeof(int64_t));
     if (speculate) {
+        std::memcpy(spec_n.data(), e->hq_n.p, nq * sizeof(int32_t));
+        if (rows) std::memcpy(rows, e->hq_rows.p, (size_t)nq * mr * sizeof(aid_match_row));
         std::vector<int> again;
         for (int q = 0; q < nq; ++q) {
             if (spec_n[q] < 0) again.push_back(q);
