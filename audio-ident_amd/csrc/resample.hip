@@ -18,6 +18,36 @@ constexpr int kResBlock = kResThreads * kResPerThread;
 
 constexpr int kResMaxLdsTaps = 12288;  // floats (48 KB): larger tables are read from L1/L2
 
+// Stage input samples lo .. lo + cnt - 1 (stream indices; src[0] is stream sample in_base, 0 outside [0, n)) into
+// sx[0 .. cnt), downmixed at load time. The loads go out kStageBatch at a time before their LDS stores: a plain
+// strided loop waits for each load before the next (its trip count is not known at compile time), so a block
+// staging ~12 samples per thread paid ~12 serial memory latencies (K6 at ~2.5 TB/s on the 256-stream push)
+constexpr int kStageBatch = 8;
+template <bool STEREO>
+__device__ __forceinline__ void stage_window(const float *__restrict__ src, int64_t lo, int64_t in_base, int64_t n,
+                                             int cnt, float *sx, int tid, int nthreads) {
+    for (int i0 = tid; i0 < cnt; i0 += kStageBatch * nthreads) {
+        float v[kStageBatch];
+#pragma unroll
+        for (int u = 0; u < kStageBatch; ++u) {
+            const int i = i0 + u * nthreads;
+            const int64_t g = lo + i - in_base;
+            v[u] = 0.0f;
+            if (i < cnt && g >= 0 && g < n) {
+                if constexpr (STEREO) {
+                    const float2 s = reinterpret_cast<const float2 *>(src)[g];
+                    v[u] = (s.x + s.y) * 0.5f;
+                } else {
+                    v[u] = src[g];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kStageBatch; ++u)
+            if (i0 + u * nthreads < cnt) sx[i0 + u * nthreads] = v[u];
+    }
+}
+
 // MODE 0: taps from L1/L2, 1: taps staged in LDS, 2: integer decimation (up == 1): one phase,
 // the taps are wave-uniform and read as scalar loads (no LDS traffic for them)
 template <bool STEREO, int MODE>
@@ -44,19 +74,7 @@ __global__ __launch_bounds__(kResThreads) void k_resample(const float *__restric
     const int64_t lo = (m0 * down + hl) / up - (J - 1);
     const int64_t hi = (mlast * down + hl) / up;  // inclusive
     const int cnt = (int)(hi - lo + 1);
-    for (int i = tid; i < cnt; i += kResThreads) {
-        const int64_t g = lo + i - in_base;
-        float v = 0.0f;
-        if (g >= 0 && g < n) {
-            if constexpr (STEREO) {
-                const float2 s = reinterpret_cast<const float2 *>(src)[g];
-                v = (s.x + s.y) * 0.5f;
-            } else {
-                v = src[g];
-            }
-        }
-        sx[i] = v;
-    }
+    stage_window<STEREO>(src, lo, in_base, n, cnt, sx, tid, kResThreads);
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kResPerThread; ++r) {
@@ -99,19 +117,7 @@ __global__ __launch_bounds__(256) void k_resample_phase(const float *__restrict_
     const int64_t lo = (m0 * down + hl) / up - (J - 1);
     const int64_t hi = (mlast * down + hl) / up;  // inclusive
     const int cnt = (int)(hi - lo + 1);
-    for (int i = tid; i < cnt; i += blockDim.x) {
-        const int64_t g = lo + i - in_base;
-        float v = 0.0f;
-        if (g >= 0 && g < n) {
-            if constexpr (STEREO) {
-                const float2 s2 = reinterpret_cast<const float2 *>(src)[g];
-                v = (s2.x + s2.y) * 0.5f;
-            } else {
-                v = src[g];
-            }
-        }
-        sx[i] = v;
-    }
+    stage_window<STEREO>(src, lo, in_base, n, cnt, sx, tid, (int)blockDim.x);
     __syncthreads();
     for (int t = tid; t < up; t += blockDim.x) {
         const int64_t c0 = (m0 + t) * down + hl;  // output r: c = c0 + r * up * down
