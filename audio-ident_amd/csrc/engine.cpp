@@ -50,6 +50,7 @@ void launch_index_scatter(const uint32_t *ph, const uint32_t *ptrack, const uint
 void launch_scan(const uint32_t *in, uint32_t *out, int64_t n, uint32_t *tmp, hipStream_t s);
 size_t index_sort_temp_bytes(int64_t n);
 bool k4_ab_sort_built();
+int match_lds_blocks_per_cu();
 size_t radix_scratch_u32(int64_t n);
 hipError_t launch_index_sort_build(const uint32_t *ph, const uint32_t *ptrack, const uint32_t *pt, int64_t n,
                                    const uint8_t *tomb, uint32_t n_tracks, uint32_t *keys0, uint32_t *keys1,
@@ -1629,9 +1630,9 @@ int aid_index_finalize(aid_engine *e) {
 int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset) {
     if (!e || (n > 0 && !out)) return fail(AID_ERR_INVALID, "aid_match_stats: bad argument");
     std::lock_guard<std::mutex> lk(e->mu);
-    const int64_t v[7] = {e->st_queries, e->st_votes,    e->st_post_reads, e->st_q_lds,
-                          e->st_q_global, e->st_records, e->st_sig_reads};
-    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+    const int64_t v[8] = {e->st_queries, e->st_votes,    e->st_post_reads, e->st_q_lds,
+                          e->st_q_global, e->st_records, e->st_sig_reads, (int64_t)match_lds_blocks_per_cu()};
+    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
     if (reset)
         e->st_queries = e->st_votes = e->st_post_reads = e->st_q_lds = e->st_q_global = e->st_records = e->st_sig_reads = 0;
     return AID_OK;

@@ -622,12 +622,10 @@ constexpr int kLdsHistBits = 15;
 constexpr int kLdsCtrBits = 8;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
-// (track, d) entries of the exact table: the music-like and synthetic catalogs hold <= 86 per window
-// (probes/spec_sweep.py statistics); a fuller table overflows to the global path
-constexpr int kFastVoteCap = 512;
-constexpr int kFastDistinctBits = 10;  // the (slot, t_q) set: <= 615 distinct per window on the same data
+constexpr int kFastVoteCap = 1024;     // (track, d) entries of the exact table
+constexpr int kFastDistinctBits = 11;  // FPSPEC v1: the (slot, t_q) set of the inserted votes, 2,048 keys
+constexpr int kFastTrackCap = 256;  // tracks with a candidate (track, d); the row staging holds 204 anyway
 constexpr int kFastDistinctCap = 1 << kFastDistinctBits;
-constexpr int kFastTrackCap = 512;
 constexpr int kFastThreads = 512;
 
 static_assert(kLdsHistBits <= 16, "the LDS filter's buckets come from 16-bit posting signatures");
@@ -778,8 +776,11 @@ __device__ __forceinline__ void sig_votes(const QueryParams &qp, int64_t a, int6
 }
 
 // hot votes queued by the insert pass (posting index, tq): the LDS the counters leave beside the exact table
-constexpr int kTableBytes = kFastVoteCap * (8 + 3 * 4) + kFastTrackCap * (4 + 8) + kFastDistinctCap * 4;
-constexpr int kHotQueue = ((1 << kLdsHistBits) / kLdsCtrPerWord * 4 - kTableBytes) / 8;
+// The union holds the 32 KB of filter counters, then the exact tables, the distinct set, the phase-3..5 counters and
+// the hot-vote queue in 36 KB: with the 4 KB hot bitmap a workgroup takes 40 KB, four per CU in the 160 KB LDS
+constexpr int kUnionBytes = 36864;
+constexpr int kTableBytes = kFastVoteCap * (8 + 3 * 4) + kFastTrackCap * (4 + 8) + kFastDistinctCap * 4 + 16;
+constexpr int kHotQueue = (kUnionBytes - kTableBytes) / 8;
 
 struct FastLds {
     union {
@@ -790,14 +791,15 @@ struct FastLds {
             uint32_t tkey[kFastTrackCap];
             unsigned long long tbest[kFastTrackCap];
             uint32_t dset[kFastDistinctCap];  // distinct (slot, t_q) of the inserted votes
+            int32_t out_n, overflow, hq_n, pad;  // phases 3-5 (the counters' LDS is free by then)
             uint2 hq[kHotQueue > 0 ? kHotQueue : 1];  // the insert pass's hot votes (posting index, tq)
         } t;
+        uint32_t bytes[kUnionBytes / 4];
     } u;
     uint32_t hot[(1 << kLdsHistBits) / 32];
-    int32_t out_n, overflow, hq_n;
 };
-static_assert(kHotQueue >= 256 && sizeof(FastLds::u) == (1 << kLdsHistBits) / kLdsCtrPerWord * 4,
-              "the hot-vote queue lives in the counters' LDS beside the exact table");
+static_assert(kHotQueue >= 512 && sizeof(FastLds::u) == kUnionBytes && sizeof(FastLds) == 40960,
+              "the hot-vote queue lives in the counters' LDS beside the exact table; 40 KB = four workgroups per CU");
 
 __global__ __launch_bounds__(kFastThreads)
 __attribute__((amdgpu_waves_per_eu(8)))
@@ -816,7 +818,6 @@ void k_match_lds(QueryParams qp) {
     const uint32_t mm = (uint32_t)qp.min_match;
     for (int i = tid; i < (1 << kLdsHistBits) / kLdsCtrPerWord; i += kFastThreads) L.u.hist[i] = 0u;
     for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
-    if (tid == 0) { L.out_n = 0; L.overflow = 0; L.hq_n = 0; }
     __syncthreads();
     // the query's exact vote total (k_query_votes): below the counter maximum no counter can wrap, so only
     // heavier queries pay for returning atomics (the carry check below)
@@ -849,10 +850,6 @@ void k_match_lds(QueryParams qp) {
         }
     });
     __syncthreads();
-    if (L.overflow) {  // uniform: the global path answers this query
-        if (tid == 0) qp.nrows[q] = -1;
-        return;
-    }
     // phase 2
     for (int w = tid; w < (1 << kLdsHistBits) / 32; w += kFastThreads) {
         uint32_t bits = 0;
@@ -877,6 +874,7 @@ void k_match_lds(QueryParams qp) {
         L.u.t.tbest[i] = 0ull;
     }
     for (int i = tid; i < kFastDistinctCap; i += kFastThreads) L.u.t.dset[i] = kDistinctEmpty;
+    if (tid == 0) { L.u.t.out_n = 0; L.u.t.overflow = 0; L.u.t.hq_n = 0; }
     __syncthreads();
     // the exact (track, d) table insert of one hot vote (slot from the full mix of (track, d))
     auto insert = [&](uint32_t tr, int32_t d, int32_t tq) {
@@ -886,13 +884,13 @@ void k_match_lds(QueryParams qp) {
         for (;;) {
             const unsigned long long old = atomicCAS(&L.u.t.vkey[s], ~0ull, key);
             if (old == ~0ull || old == key) {
-                if (distinct_first(L.u.t.dset, kFastDistinctBits, s, (uint32_t)tq, &L.overflow))
+                if (distinct_first(L.u.t.dset, kFastDistinctBits, s, (uint32_t)tq, &L.u.t.overflow))
                     atomicAdd(&L.u.t.vcnt[s], 1u);
                 atomicMin(&L.u.t.vmin[s], (uint32_t)tq);
                 atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
                 break;
             }
-            if (++probes >= kProbeMax) { L.overflow = 1; break; }
+            if (++probes >= kProbeMax) { L.u.t.overflow = 1; break; }
             s = (s + 1) & (kFastVoteCap - 1);
         }
     };
@@ -917,7 +915,7 @@ void k_match_lds(QueryParams qp) {
                 const int e = __builtin_ctz(hm[u]);
                 hm[u] &= hm[u] - 1;
                 const uint32_t pi = (uint32_t)kSigChunk * cid[u] + (uint32_t)e;
-                const int slot = atomicAdd(&L.hq_n, 1);
+                const int slot = atomicAdd(&L.u.t.hq_n, 1);
                 if (slot < kHotQueue) {
                     L.u.t.hq[slot] = make_uint2(pi, (uint32_t)tqs[u]);
                 } else {  // queue full: this vote's posting now (a dependent load: one memory latency)
@@ -933,7 +931,7 @@ void k_match_lds(QueryParams qp) {
     // the queued hot votes: every thread loads its entries' postings at once (one memory latency for the whole
     // queue instead of one per hot vote inside the walk), then inserts them
     {
-        const int nh = min(L.hq_n, kHotQueue);
+        const int nh = min(L.u.t.hq_n, kHotQueue);
         for (int i = tid; i < nh; i += kFastThreads) {
             const uint2 h = L.u.t.hq[i];
             const uint64_t pv = qp.post[h.x];
@@ -957,7 +955,7 @@ void k_match_lds(QueryParams qp) {
                 atomicMax(&L.u.t.tbest[t], packed);
                 break;
             }
-            if (++probes >= kFastTrackCap) { L.overflow = 1; break; }
+            if (++probes >= kFastTrackCap) { L.u.t.overflow = 1; break; }
             t = (t + 1) & (kFastTrackCap - 1);
         }
     }
@@ -973,7 +971,7 @@ void k_match_lds(QueryParams qp) {
         uint32_t t = (tr * 0x9E3779B1u >> 22) & (kFastTrackCap - 1);
         for (int probes = 0; probes < kFastTrackCap && L.u.t.tkey[t] != tr; ++probes) t = (t + 1) & (kFastTrackCap - 1);
         if (L.u.t.tkey[t] == tr && L.u.t.tbest[t] == packed) {
-            const int o = atomicAdd(&L.out_n, 1);
+            const int o = atomicAdd(&L.u.t.out_n, 1);
             if (o < kRowCap) {
                 rowbuf[o][0] = (int32_t)L.u.t.vcnt[s];
                 rowbuf[o][1] = (int32_t)tr;
@@ -984,7 +982,7 @@ void k_match_lds(QueryParams qp) {
         }
     }
     __syncthreads();
-    const int nr = min(L.out_n, kRowCap);
+    const int nr = min(L.u.t.out_n, kRowCap);
     for (int i = tid; i < nr; i += kFastThreads) {
         int rank = 0;
         for (int j = 0; j < nr; ++j) {
@@ -998,7 +996,7 @@ void k_match_lds(QueryParams qp) {
             for (int c = 0; c < 5; ++c) o[c] = rowbuf[i][c];
         }
     }
-    if (tid == 0) qp.nrows[q] = (L.overflow || L.out_n > kRowCap) ? -1 : min(nr, qp.max_rows);
+    if (tid == 0) qp.nrows[q] = (L.u.t.overflow || L.u.t.out_n > kRowCap) ? -1 : min(nr, qp.max_rows);
 }
 
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,
@@ -1009,6 +1007,13 @@ void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t
     QueryParams qp{recs, qstart, qcount, nq, offsets, post, tomb, n_tracks, min_match, max_rows, nullptr, 0, rows, nrows,
                    tomb_live, nullptr, 1, votes, sig, ranges};
     timed_launch(k_match_lds, dim3(nq), dim3(kFastThreads), 0, s, qp);
+}
+
+// resident k_match_lds workgroups per CU (LDS- and register-limited; 4 by design), for the match statistics
+int match_lds_blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_match_lds, kFastThreads, 0) != hipSuccess) n = -1;
+    return n;
 }
 
 void launch_index_count(const uint32_t *ph, const uint32_t *ptrack, int64_t n, const uint8_t *tomb, uint32_t n_tracks,

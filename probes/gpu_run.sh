@@ -3,7 +3,8 @@
 #   tests  the whole -m gpu suite        smoke  __graft_entry__.smoke()
 #   bench  the default bench.py line     music  probes/music_eval.py (1,000 songs, 8 degradation categories)
 #   prof   rocprofv3 --kernel-trace --stats of the headline-only bench
-#   pmc    the headline's FETCH_SIZE / WRITE_SIZE passes and the two SQ passes (tools/prof_summary.py inputs)
+#   pmc    the headline's kernel trace, FETCH_SIZE / WRITE_SIZE and SQ passes (profiles/run_rocprof.sh, run_sq.sh:
+#          gpurun_out/prof_TAG, gpurun_out/sq_TAG, the inputs of tools/prof_summary.py TAG)
 #   k5     the config-4 lane (catalog leg): kernel trace, FETCH_SIZE, WRITE_SIZE (tools/k5_pmc_summary.py inputs)
 #   k5req  the lane's memory-side read requests by size (TCC_EA0_RDREQ, TCC_EA0_RDREQ_32B) and TCP->TCC reads
 #   segv   VERDICT r5 #2: the r05y2 command (service leg under --kernel-trace --memory-copy-trace), once
@@ -26,12 +27,7 @@ for step in "$@"; do
     bench) timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err ;;
     music) timeout -k 10 900 python3 -u probes/music_eval.py --tracks 1000 --queries 500 --negatives 100 --workers 16 > $O/music.json 2> $O/music.err ;;
     prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --no-catalog --no-stream --no-service > $O/prof_bench.json 2> $O/prof.err ;;
-    pmc)
-      H="python3 bench.py --steps 5 --warmup 1 --settle 0 --no-cpu --no-fullband --no-catalog --no-service --no-stream"
-      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $O/pmc/fetch -o run --output-format csv -- $H > $O/pmc_fetch.log 2>&1 &&
-      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $O/pmc/write -o run --output-format csv -- $H > $O/pmc_write.log 2>&1 &&
-      timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -T -d $O/pmc/sq1 -o run --output-format csv -- $H > $O/pmc_sq1.log 2>&1 &&
-      timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU -T -d $O/pmc/sq2 -o run --output-format csv -- $H > $O/pmc_sq2.log 2>&1 ;;
+    pmc) bash profiles/run_rocprof.sh $TAG > $O/pmc_prof.log 2>&1 && bash profiles/run_sq.sh $TAG > $O/pmc_sq.log 2>&1 ;;
     k5)
       B="python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-service --no-stream"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $O/k5/trace -o run --output-format csv -- $B > $O/k5_trace.json 2> $O/k5_trace.err &&

@@ -83,3 +83,12 @@ def test_mixed_batch_routes_each_query_by_its_votes():
         votes_heavy = len(qrec) * per_hash
         assert votes_heavy > (1 << 18)
         assert st["queries_global"] == 2 and st["queries_lds"] == len(qs) - 2, st
+
+
+def test_lds_path_keeps_four_workgroups_per_cu():
+    """k_match_lds is laid out for exactly 40 KB of LDS (FPSPEC v1's distinct-frame set included): four resident
+    workgroups per CU, the occupancy its timing was tuned at."""
+    from aidfp.engine import Engine
+
+    with Engine(44100) as eng:
+        assert eng.match_stats()["lds_path_workgroups_per_cu"] == 4
