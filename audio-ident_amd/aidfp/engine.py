@@ -385,10 +385,11 @@ class Engine:
 
     def match_stats(self, reset: bool = False) -> dict:
         """Cumulative K5 counters (aid_match_stats): queries, votes, postings read, path split, records."""
-        out = np.zeros(8, dtype=np.int64)
-        check(self._lib.aid_match_stats(self._h, _p(out), 8, 1 if reset else 0))
+        out = np.zeros(13, dtype=np.int64)
+        check(self._lib.aid_match_stats(self._h, _p(out), 13, 1 if reset else 0))
         return dict(zip(("queries", "votes", "posting_reads", "queries_lds", "queries_global", "records", "sig_reads",
-                         "lds_path_workgroups_per_cu"), (int(x) for x in out)))
+                         "lds_path_workgroups_per_cu", "fallback_heavy", "fallback_table", "fallback_distinct",
+                         "fallback_tracks", "fallback_rows"), (int(x) for x in out)))
 
     # ---- PCM front-end (FPSPEC 8): downmix + resample, device buffers ----
     def resample_len(self, n: int, sr_in: int, sr_out: int) -> int:

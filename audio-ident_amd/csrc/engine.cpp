@@ -280,6 +280,7 @@ struct aid_engine {
     // aid_match_stats: queries, exact votes, and the postings K5 read (a vote = one 8-B posting per pass)
     int64_t st_queries = 0, st_votes = 0, st_post_reads = 0, st_q_global = 0, st_q_lds = 0, st_records = 0;
     int64_t st_sig_reads = 0;  // 2-B posting signatures the LDS path read (two per vote: counting and insert passes)
+    int64_t st_fb_reason[5] = {0, 0, 0, 0, 0};  // LDS-path fallbacks (speculative pass) by reason (index.hip)
     int64_t tomb_since_build = 0;  // removals after the last CSR build (queries must check tomb[])
     size_t k5_batch = 2048;        // global-path queries per launch
     hipStream_t last_stream = nullptr;
@@ -1630,11 +1631,15 @@ int aid_index_finalize(aid_engine *e) {
 int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset) {
     if (!e || (n > 0 && !out)) return fail(AID_ERR_INVALID, "aid_match_stats: bad argument");
     std::lock_guard<std::mutex> lk(e->mu);
-    const int64_t v[8] = {e->st_queries, e->st_votes,    e->st_post_reads, e->st_q_lds,
-                          e->st_q_global, e->st_records, e->st_sig_reads, (int64_t)match_lds_blocks_per_cu()};
-    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
-    if (reset)
+    const int64_t v[13] = {e->st_queries,     e->st_votes,   e->st_post_reads, e->st_q_lds,
+                           e->st_q_global,    e->st_records, e->st_sig_reads,  (int64_t)match_lds_blocks_per_cu(),
+                           e->st_fb_reason[0], e->st_fb_reason[1], e->st_fb_reason[2], e->st_fb_reason[3],
+                           e->st_fb_reason[4]};
+    for (int i = 0; i < n && i < 13; ++i) out[i] = v[i];
+    if (reset) {
         e->st_queries = e->st_votes = e->st_post_reads = e->st_q_lds = e->st_q_global = e->st_records = e->st_sig_reads = 0;
+        for (auto &r : e->st_fb_reason) r = 0;
+    }
     return AID_OK;
 }
 
@@ -2137,8 +2142,12 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
         if (rows) std::memcpy(rows, e->hq_rows.p, (size_t)nq * mr * sizeof(aid_match_row));
         std::vector<int> again;
         for (int q = 0; q < nq; ++q) {
-            if (spec_n[q] < 0) again.push_back(q);
-            else nrows[q] = spec_n[q];
+            if (spec_n[q] < 0) {
+                again.push_back(q);
+                ++e->st_fb_reason[std::min(-spec_n[q], 5) - 1];
+            } else {
+                nrows[q] = spec_n[q];
+            }
         }
         todo.swap(again);
         e->n_fallback += (int64_t)todo.size();

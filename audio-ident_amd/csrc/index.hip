@@ -63,7 +63,7 @@ __device__ __forceinline__ bool distinct_first(uint32_t *set, int bits, uint32_t
         if (old == key) return false;
         i = (i + 1) & mask;
     }
-    *overflow = 1;
+    atomicMax(overflow, 3);  // K5 fallback reason 3: the distinct set is full
     return false;
 }
 
@@ -890,7 +890,7 @@ void k_match_lds(QueryParams qp) {
                 atomicMax(&L.u.t.vmax[s], (uint32_t)tq);
                 break;
             }
-            if (++probes >= kProbeMax) { L.u.t.overflow = 1; break; }
+            if (++probes >= kProbeMax) { atomicMax(&L.u.t.overflow, 2); break; }  // reason 2: (track, d) table
             s = (s + 1) & (kFastVoteCap - 1);
         }
     };
@@ -955,7 +955,7 @@ void k_match_lds(QueryParams qp) {
                 atomicMax(&L.u.t.tbest[t], packed);
                 break;
             }
-            if (++probes >= kFastTrackCap) { L.u.t.overflow = 1; break; }
+            if (++probes >= kFastTrackCap) { atomicMax(&L.u.t.overflow, 4); break; }  // reason 4: track table
             t = (t + 1) & (kFastTrackCap - 1);
         }
     }
@@ -996,7 +996,10 @@ void k_match_lds(QueryParams qp) {
             for (int c = 0; c < 5; ++c) o[c] = rowbuf[i][c];
         }
     }
-    if (tid == 0) qp.nrows[q] = (L.u.t.overflow || L.u.t.out_n > kRowCap) ? -1 : min(nr, qp.max_rows);
+    // a query the LDS path cannot answer reports -(reason): 1 above kLdsMaxVotes, 2 (track, d) table, 3 distinct set,
+    // 4 track table, 5 more rows than the staging holds (the engine re-runs it on the global path and counts reasons)
+    if (tid == 0)
+        qp.nrows[q] = L.u.t.overflow ? -L.u.t.overflow : L.u.t.out_n > kRowCap ? -5 : min(nr, qp.max_rows);
 }
 
 void launch_match_lds(const uint64_t *recs, const int64_t *qstart, const int64_t *qcount, int nq,

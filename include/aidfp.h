@@ -205,7 +205,9 @@ int aid_index_finalize(aid_engine *e);
    hash a query record hits), [2] 8-B postings K5's global path read (once per key partition in K5a + once in K5b),
    [3] queries answered on the LDS path, [4] on the global path, [5] query records, [6] 2-B posting signatures the
    LDS path read (twice per vote: its counting and insert passes; the insert pass also reads the 8-B posting of a
-   vote whose bucket is hot), [7] resident LDS-path workgroups per CU (an occupancy query, not a counter). */
+   vote whose bucket is hot), [7] resident LDS-path workgroups per CU (an occupancy query, not a counter),
+   [8..12] queries the LDS path handed to the global path, by reason: above 2^18 votes, (track, d) table full,
+   distinct-frame set full, track table full, more rows than its staging holds. */
 int aid_match_stats(aid_engine *e, int64_t *out, int32_t n, int32_t reset);
 /* n_postings = stored postings, n_live = postings in the built CSR (-1 if stale), n_tracks = max id + 1 */
 int aid_index_stats(aid_engine *e, int64_t *n_postings, int64_t *n_live, uint32_t *n_tracks);

@@ -499,3 +499,30 @@ def test_async_append_equals_per_clip_records(tmp_path):
         recs = eng.extract_host([synth.synth(7, 0, 4 * sr, sr), synth.synth(8, 0, 5 * sr, sr)])
         eng.index_add_extracted(np.array([7, 8], np.uint32))
         assert np.array_equal(eng.index_export(), np.concatenate([rows(7, recs[0]), rows(8, recs[1])]))
+
+
+@pytest.mark.parametrize("path", [0, 1, 2])
+def test_match_v1_golden_fixture_on_gpu(path):
+    """The committed FPSPEC v1 match vectors (tests/golden/oracle_match_v1.*) through the engine: the fixture's postings
+    added as raw postings, its query records matched on the automatic, LDS and global paths -- rows equal the
+    fixture's (distinct anchor frames, min_match 10)."""
+    import json
+    from pathlib import Path
+
+    gdir = Path(__file__).resolve().parent / "golden"
+    g = np.load(gdir / "oracle_match_v1.npz")
+    meta = json.loads((gdir / "oracle_match_v1.json").read_text())
+    post = np.ascontiguousarray(g["postings"])
+    eng = Engine(meta["sr"])
+    try:
+        h, t, tm = (np.ascontiguousarray(post[:, k]) for k in range(3))
+        eng.index_add_postings(h.ctypes.data, t.ctypes.data, tm.ctypes.data, len(post), device=False)
+        eng.index_finalize()
+        if path:
+            eng.force("k5_path", path)
+        recs = [g[f"rec_{i}"] for i in range(len(meta["queries"]))]
+        got = eng.query(recs)
+        for i, r in enumerate(got):
+            assert np.array_equal(r, g[f"rows_mm10_{i}"]), (i, r, g[f"rows_mm10_{i}"])
+    finally:
+        eng.close()

@@ -5,7 +5,8 @@ the oracle is pinned here by:
   * float64 numpy rfft power (tolerance);
   * the literal FPSPEC 5 peak definition (brute force) vs the separable form;
   * known-answer cases (bin-centred sinusoids, hand-built peak lists);
-  * the committed golden fixture tests/golden/oracle_v0.npz (regression lock).
+  * the committed golden fixtures tests/golden/oracle_v0.npz (extraction) and oracle_match_v1.npz (FPSPEC v1
+    match: distinct anchor frames), as regression locks.
 """
 
 import json
@@ -150,3 +151,21 @@ def test_numpy_scipy_path_matches_on_synthetic_clips():
     for tr, snr, fmax in ((3, None, 8000), (4, 20.0, 8000), (5, None, 20000)):
         x = synth.synth(tr, 0, 44100 * 4, 44100, snr_db=snr, fmax_hz=fmax)
         assert np.array_equal(O.fingerprint_numpy(x, 512), O.fingerprint(x, 512))
+
+
+def test_match_v1_golden_fixture():
+    """FPSPEC v1 section 7 regression vectors (tests/golden/make_match_golden.py): the oracle's rows from the committed
+    postings and query records at min_match 10 and 4; every v1 score is at most the v0 vote count of its (track, d),
+    and the two differ (what v1 changed)."""
+    g = np.load(GOLDEN / "oracle_match_v1.npz")
+    meta = json.loads((GOLDEN / "oracle_match_v1.json").read_text())
+    post = g["postings"]
+    differ = 0
+    for i in range(len(meta["queries"])):
+        rec = g[f"rec_{i}"]
+        for mm in (10, 4):
+            assert np.array_equal(O.query(post, rec, min_match=mm, max_rows=50), g[f"rows_mm{mm}_{i}"]), (i, mm)
+        rows, v0 = g[f"rows_mm4_{i}"], g[f"v0votes_{i}"]
+        assert (rows[:, 0] <= v0).all() if len(rows) else True
+        differ += int((rows[:, 0] < v0).sum()) if len(rows) else 0
+    assert differ > 0
