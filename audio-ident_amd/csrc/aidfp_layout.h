@@ -76,8 +76,8 @@ __host__ __device__ constexpr uint16_t posting_sig(uint32_t track, uint32_t t) {
 }
 
 // K5: the heaviest query (exact votes, k_query_votes) the LDS match path takes; heavier ones go straight to the
-// global-histogram path (engine.cpp run_queries routes them, k_match_lds hands any back at once). 8 votes per
-// counter of its 2^15-bucket filter: on config 4 (~84.5 k votes per window, a few up to ~2^18) every query stays in
+// global-histogram path (engine.cpp run_queries routes them, k_match_lds hands any back at once). 4 votes per
+// counter of its 2^16-bucket filter (2^15 8-bit counters before round 6, 8 per counter): on config 4 (~84.5 k votes per window, a few up to ~2^18) every query stays in
 // LDS, where the 132 of 36,864 heaviest ones had cost 0.3 ms per 4096-clip call on the global path at 2^17.
 constexpr int64_t kLdsMaxVotes = (int64_t)1 << 18;
 

@@ -2182,7 +2182,7 @@ static int run_queries(aid_engine *e, const uint64_t *recs, const int64_t *qstar
     // 185k clips/s, rows equal), so a batch goes to it when its mean query has <= 2^17 votes (2 per counter) and
     // none has more than 2^20 (a heavier one falls back to the global path after its LDS run)
     // Each query is routed by its own vote count: k_match_lds answers the queries with <= kLdsMaxVotes
-    // (2^18 votes over the 2^15 8-bit counters of its filter = 8 per counter, aidfp_layout.h) and hands heavier ones
+    // (2^18 votes over the 2^16 4-bit counters of its filter = 4 per counter, aidfp_layout.h) and hands heavier ones
     // straight back (nrows -1, no LDS run), so the batch takes
     // the LDS launch whenever some query is light enough for it; the heavy ones run on the global path below
     int n_light = 0;

@@ -618,10 +618,18 @@ __global__ __launch_bounds__(1024) void k_vote_final(QueryParams qp) {
 // -> 4-posting chunks 2.71-2.76 -> hot-vote queue 2.68 -> 8-posting chunks, four 512-thread workgroups per CU, the
 // LDS path up to 2^18 votes per query 1.80-1.86.
 constexpr int kLdsSigWindows = 3;  // windows of 64 two-byte signature loads a wave keeps in flight
-constexpr int kLdsHistBits = 15;
-constexpr int kLdsCtrBits = 8;
+// The filter: 2^16 4-bit counters in 32 KB (round 6; 2^15 8-bit counters before). FPSPEC v1's min_match 10 had made
+// the 8-bit filter's chance-hot buckets ~20x more frequent than at 12 (a Poisson tail at ~2.6 votes per bucket on
+// config 4), and 11 % of config-4 windows overflowed the exact table; twice the buckets halve the load per counter.
+// A counter that wraps (>= 16 votes) marks its bucket hot, so the filter stays an exact superset for any min_match.
+// The hot bitmap holds one bit per PAIR of buckets (2^15 bits, 4 KB as before): a hot bucket makes its pair
+// neighbour a candidate too (still a superset).
+constexpr int kLdsHistBits = 16;
+constexpr int kLdsCtrBits = 4;
 constexpr int kLdsCtrPerWord = 32 / kLdsCtrBits;
 constexpr uint32_t kLdsCtrMax = (1u << kLdsCtrBits) - 1;
+constexpr int kHotShift = 1;                              // buckets per hot bit = 2^kHotShift
+constexpr int kHotWords = (1 << (kLdsHistBits - kHotShift)) / 32;
 constexpr int kFastVoteCap = 1024;     // (track, d) entries of the exact table
 constexpr int kFastDistinctBits = 11;  // FPSPEC v1: the (slot, t_q) set of the inserted votes, 2,048 keys
 constexpr int kFastTrackCap = 256;  // tracks with a candidate (track, d); the row staging holds 204 anyway
@@ -796,7 +804,7 @@ struct FastLds {
         } t;
         uint32_t bytes[kUnionBytes / 4];
     } u;
-    uint32_t hot[(1 << kLdsHistBits) / 32];
+    uint32_t hot[kHotWords];
 };
 static_assert(kHotQueue >= 512 && sizeof(FastLds::u) == kUnionBytes && sizeof(FastLds) == 40960,
               "the hot-vote queue lives in the counters' LDS beside the exact table; 40 KB = four workgroups per CU");
@@ -804,7 +812,7 @@ static_assert(kHotQueue >= 512 && sizeof(FastLds::u) == kUnionBytes && sizeof(Fa
 __global__ __launch_bounds__(kFastThreads)
 __attribute__((amdgpu_waves_per_eu(8)))
 void k_match_lds(QueryParams qp) {
-    __shared__ FastLds L;  // 2^15 8-bit counters + the exact table / hot-vote queue: 36 KB, four workgroups per CU
+    __shared__ FastLds L;  // 2^16 4-bit counters, then the exact tables / hot-vote queue; 40 KB, four workgroups per CU
     const int q = blockIdx.x;
     // a query heavier than the LDS filter suits goes to the global path at once, by its own vote count (a heavy
     // query here would wrap many 8-bit counters, mark their buckets hot and likely overflow the exact table after a
@@ -817,7 +825,7 @@ void k_match_lds(QueryParams qp) {
     const int64_t a = qp.qstart[q], n = qp.qcount[q];
     const uint32_t mm = (uint32_t)qp.min_match;
     for (int i = tid; i < (1 << kLdsHistBits) / kLdsCtrPerWord; i += kFastThreads) L.u.hist[i] = 0u;
-    for (int i = tid; i < (1 << kLdsHistBits) / 32; i += kFastThreads) L.hot[i] = 0u;
+    for (int i = tid; i < kHotWords; i += kFastThreads) L.hot[i] = 0u;
     __syncthreads();
     // the query's exact vote total (k_query_votes): below the counter maximum no counter can wrap, so only
     // heavier queries pay for returning atomics (the carry check below)
@@ -831,19 +839,22 @@ void k_match_lds(QueryParams qp) {
     }
 
     // phase 1: every vote counted from its posting's 2-B signature alone (bucket = sig - tq = H(track) + d)
+    auto mark_hot = [&](uint32_t b) {
+        const uint32_t hb = b >> kHotShift;
+        atomicOr(&L.hot[hb >> 5], 1u << (hb & 31));
+    };
     sig_votes(qp, a, n, wave, nw, lane, one_group, grp_one, [&](uint32_t h) {
         const uint32_t sh = kLdsCtrBits * (h % kLdsCtrPerWord);
         uint32_t *w = &L.u.hist[h / kLdsCtrPerWord];
         if (check_wrap) {
             const uint32_t old = atomicAdd(w, 1u << sh);
             if (((old >> sh) & kLdsCtrMax) == kLdsCtrMax) {
-                // wrapped: the bucket holds >= 256 votes, so it is hot whatever its counter ends at;
+                // wrapped: the bucket holds > kLdsCtrMax votes, so it is hot whatever its counter ends at;
                 // the carry went on into the next counters of the word, and through each full one
-                atomicOr(&L.hot[h >> 5], 1u << (h & 31));
-                for (uint32_t j = h % 4 + 1; j < 4 && ((old >> (8 * j)) & 0xFFu) == 0xFFu; ++j) {
-                    const uint32_t hj = (h & ~3u) + j;
-                    atomicOr(&L.hot[hj >> 5], 1u << (hj & 31));
-                }
+                mark_hot(h);
+                for (uint32_t j = h % kLdsCtrPerWord + 1;
+                     j < kLdsCtrPerWord && ((old >> (kLdsCtrBits * j)) & kLdsCtrMax) == kLdsCtrMax; ++j)
+                    mark_hot((h & ~(uint32_t)(kLdsCtrPerWord - 1)) + j);
             }
         } else {
             atomicAdd(w, 1u << sh);
@@ -851,14 +862,16 @@ void k_match_lds(QueryParams qp) {
     });
     __syncthreads();
     // phase 2
-    for (int w = tid; w < (1 << kLdsHistBits) / 32; w += kFastThreads) {
+    // phase 2: hot bit of a bucket pair = either counter >= min_match (a hot word covers 32 pairs = 8 counter words)
+    constexpr int kPairsPerWord = kLdsCtrPerWord >> kHotShift;
+    for (int w = tid; w < kHotWords; w += kFastThreads) {
         uint32_t bits = 0;
 #pragma unroll
-        for (int j = 0; j < 32 / kLdsCtrPerWord; ++j) {
-            const uint32_t v = L.u.hist[w * (32 / kLdsCtrPerWord) + j];
+        for (int j = 0; j < 32 / kPairsPerWord; ++j) {
+            const uint32_t v = L.u.hist[w * (32 / kPairsPerWord) + j];
 #pragma unroll
             for (int b = 0; b < kLdsCtrPerWord; ++b)
-                bits |= (uint32_t)(((v >> (kLdsCtrBits * b)) & kLdsCtrMax) >= mm) << (kLdsCtrPerWord * j + b);
+                bits |= (uint32_t)(((v >> (kLdsCtrBits * b)) & kLdsCtrMax) >= mm) << (kPairsPerWord * j + (b >> kHotShift));
         }
         L.hot[w] |= bits;  // with the buckets phase 1 found wrapped
     }
@@ -878,6 +891,9 @@ void k_match_lds(QueryParams qp) {
     __syncthreads();
     // the exact (track, d) table insert of one hot vote (slot from the full mix of (track, d))
     auto insert = [&](uint32_t tr, int32_t d, int32_t tq) {
+        // once some table is full the query goes to the global path anyway: later inserts would each probe a full
+        // table (512 slots, or the whole 2,048-key distinct set) for nothing
+        if (*(volatile int32_t *)&L.u.t.overflow) return;
         const unsigned long long key = ((unsigned long long)tr << 32) | (uint32_t)d;
         uint32_t s = (mix_td(tr, d) >> 20) & (kFastVoteCap - 1);
         int probes = 0;
@@ -906,7 +922,8 @@ void k_match_lds(QueryParams qp) {
 #pragma unroll
             for (int e = 0; e < kSigChunk; ++e) {
                 const uint32_t h = sig_bucket(sw[u], e, tqs[u]);
-                hm[u] |= ((vm[u] >> e) & (L.hot[h >> 5] >> (h & 31)) & 1u) << e;
+                const uint32_t hb = h >> kHotShift;
+                hm[u] |= ((vm[u] >> e) & (L.hot[hb >> 5] >> (hb & 31)) & 1u) << e;
             }
         }
 #pragma unroll
