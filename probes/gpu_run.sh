@@ -11,6 +11,8 @@
 #   counters  rocprofv3 -L
 #   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/k2pf2 (probes/run_ab_lib.sh, 3 rounds)
 #   svcab  the service leg with 1 vs 2 coalescer dispatcher threads, interleaved, 2 rounds
+#   streamprof  probes/stream_host_profile.py (256 streams: push wall time, GPU kernels per push, cProfile)
+#   streamtrace the same probe under rocprofv3 --runtime-trace --kernel-trace (HIP API durations: host waits)
 #   k5mm   config 4 (bench_match.py, 100k tracks, 10k + 1k clips) at engine min_match 10 and 12: K5 time, fallbacks
 # Every step has its own time limit; the first failing step ends the run (exit 10 + step number).
 set -o pipefail
@@ -40,6 +42,8 @@ for step in "$@"; do
     segv) timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/segv.json 2> $O/segv.err ;;
     counters) timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 ;;
     k2ab) timeout -k 10 900 bash probes/run_ab_lib.sh $O/k2pf2_ab.txt k2pf2 3 > $O/k2ab.log 2>&1 ;;
+    streamprof) timeout -k 10 300 python3 probes/stream_host_profile.py > $O/stream_prof.txt 2> $O/stream_prof.err ;;
+    streamtrace) timeout -k 10 300 rocprofv3 --runtime-trace --kernel-trace --stats -T -d $O/strace -o run --output-format csv -- python3 probes/stream_host_profile.py --seconds 30 > $O/stream_trace.txt 2> $O/stream_trace.err ;;
     k5mm)
       timeout -k 10 400 python3 bench_match.py --no-cpu --category-queries 200 --min-match 10 > $O/k5mm10.json 2> $O/k5mm10.err &&
       timeout -k 10 400 python3 bench_match.py --no-cpu --category-queries 200 --min-match 12 > $O/k5mm12.json 2> $O/k5mm12.err ;;
