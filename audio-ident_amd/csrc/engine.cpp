@@ -235,6 +235,7 @@ struct aid_engine {
     HostBuf<int64_t> hq_meta;   // run_queries: per query start, record count, exact votes (pinned: async D2H)
     HostBuf<int32_t> hq_n;      // run_queries: the LDS path's per-query row counts
     HostBuf<int32_t> hq_rows;   // run_queries: the LDS path's rows, [nq][max_results][5]
+    HostBuf<int64_t> hq_start;  // the queries' record starts (clip_base) staged page-locked for their upload
     DevBuf<int64_t> q_votes;  // exact votes per query (LDS-histogram eligibility)
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
@@ -516,6 +517,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->hq_meta.release();
     e->hq_n.release();
     e->hq_rows.release();
+    e->hq_start.release();
     e->q_rows.release();
     e->q_nrows.release();
     e->x_src.release();
@@ -2339,6 +2341,16 @@ int aid_query(aid_engine *e, const aid_hash *recs, const int64_t *qoff, int32_t 
     return run_queries(e, e->q_recs.p, e->q_start.p, e->q_count.p, nq, std::max<int64_t>(n, 1), rows, nrows, s);
 }
 
+// q_start <- clip_base through page-locked staging: from the engine's std::vector (pageable) the copy could hold
+// the host until the stream had drained the extraction queued before it. Every caller waits for its stream before
+// returning, so the staging is free again at the next call.
+static hipError_t upload_clip_base(aid_engine *e, int n, hipStream_t s) {
+    hipError_t he = e->hq_start.reserve((size_t)n);
+    if (he != hipSuccess) return he;
+    std::memcpy(e->hq_start.p, e->clip_base.data(), (size_t)n * sizeof(int64_t));
+    return hipMemcpyAsync(e->q_start.p, e->hq_start.p, (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, s);
+}
+
 static int query_extracted_locked(aid_engine *e, aid_match_row *rows, int32_t *nrows) {
     if (int rc = check_query_frames(e)) return rc;
     if (int rc = ensure_index(e)) return rc;
@@ -2347,7 +2359,7 @@ static int query_extracted_locked(aid_engine *e, aid_match_row *rows, int32_t *n
     if (nq == 0) return AID_OK;
     if (!rows || !nrows) return fail(AID_ERR_INVALID, "null output");
     HIP_TRY(e->q_start.reserve(nq));
-    HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(upload_clip_base(e, nq, s));
     return run_queries(e, e->records.p, e->q_start.p, e->counts.p, nq, (int64_t)e->records.n, rows, nrows, s);
 }
 
@@ -2512,7 +2524,7 @@ static int exact_lane_locked(aid_engine *e, const float *pcm, const int64_t *off
         }
         if (int rc = check_query_frames(e)) return rc;
         HIP_TRY(e->q_start.reserve(n_win));
-        HIP_TRY(hipMemcpyAsync(e->q_start.p, e->clip_base.data(), n_win * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(upload_clip_base(e, n_win, s));
         if (int rc = run_queries(e, e->records.p, e->q_start.p, e->counts.p, n_win, (int64_t)e->records.n, nullptr,
                                  nrows.data(), s))
             return rc;
