@@ -577,6 +577,16 @@ class Engine:
         self.n_clips = nq
         return self._rows(rows, nrows, nq)
 
+    def query_windows_submit(self, pcm_ptr: int, starts, ends, stream: int | None = None) -> "PendingQuery":
+        """query_windows in two halves (aid_query_windows_submit): the extraction, K5 and the result copies are queued
+        on `stream` and a PendingQuery is returned at once; its collect() waits for them and returns the rows."""
+        st = np.ascontiguousarray(starts, dtype=np.int64)
+        en = np.ascontiguousarray(ends, dtype=np.int64)
+        t = ctypes.c_void_p()
+        check(self._lib.aid_query_windows_submit(self._h, ctypes.c_void_p(pcm_ptr), _p(st), _p(en), len(st),
+                                                 ctypes.c_void_p(stream) if stream else None, ctypes.byref(t)))
+        return PendingQuery(self, t, len(st))
+
     # -- batched exact lane --
     EXACT_DTYPE = np.dtype([("track", "<u4"), ("aligned_hashes", "<i4"), ("offset_seconds", "<f8"),
                             ("confidence", "<f8")])
@@ -652,3 +662,30 @@ def peaks_from_mask(mask: np.ndarray) -> np.ndarray:
 
 
 __all__ = ["Engine", "EngineError", "EngineUnavailable", "peaks_from_mask"]
+
+
+class PendingQuery:
+    """A submitted aid_query_windows_submit ticket; collect() once (a dropped one is collected and discarded)."""
+
+    __slots__ = ("eng", "ticket", "nq")
+
+    def __init__(self, eng: "Engine", ticket: ctypes.c_void_p, nq: int):
+        self.eng, self.ticket, self.nq = eng, ticket, nq
+
+    def collect(self) -> list[np.ndarray]:
+        if self.ticket is None:
+            raise RuntimeError("ticket already collected")
+        t, self.ticket = self.ticket, None
+        nq = self.nq
+        mr = self.eng.max_results
+        rows = (AidMatchRow * max(1, nq * mr))()
+        nrows = np.zeros(max(1, nq), dtype=np.int32)
+        check(self.eng._lib.aid_query_windows_collect(self.eng._h, t, ctypes.addressof(rows), _p(nrows)))
+        return self.eng._rows(rows, nrows[:nq], nq) if nq else []
+
+    def __del__(self):  # pragma: no cover - an abandoned ticket still frees its buffers
+        if getattr(self, "ticket", None) is not None and not _finalizing():
+            try:
+                self.collect()
+            except Exception:
+                pass

@@ -241,6 +241,16 @@ class StreamBank:
     def push(self, chunk) -> list[list[WindowResult]]:
         """chunk: [S, n, 2] float32 at stream_sr (device tensor or host array). Returns, per stream, the windows this
         push completed (the same start times in every stream)."""
+        return self._push(chunk, False)
+
+    def push_submit(self, chunk) -> "PendingPush":
+        """push() in two halves: the chunk's append and K6, then the extraction and match of the windows it completed
+        are QUEUED (aid_query_windows_submit) and a PendingPush is returned at once; its collect() gives push()'s result.
+        A serving loop submits push N + 1 before it collects push N, so the host work of one overlaps the kernels of
+        the other."""
+        return self._push(chunk, True)
+
+    def _push(self, chunk, submit: bool):
         import torch
 
         n = int(chunk.shape[1])
@@ -277,11 +287,32 @@ class StreamBank:
         if not starts:
             if self.timings is not None:
                 self.timings.append((t1 - t0, t2 - t1, 0.0))
-            return [[] for _ in range(self.S)]
+            return PendingPush(None, [], self.S, self.sr) if submit else [[] for _ in range(self.S)]
         rel = np.array(starts, dtype=np.int64) - self.base
         ws = (np.arange(self.S, dtype=np.int64)[:, None] * self.cap_m + rel[None, :]).ravel()
+        if submit:
+            pend = self.eng.query_windows_submit(self.mono.data_ptr(), ws, ws + self.win, s)
+            if self.timings is not None:
+                self.timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
+            return PendingPush(pend, starts, self.S, self.sr)
         rows = self.eng.query_windows(self.mono.data_ptr(), ws, ws + self.win, s)
         if self.timings is not None:
             self.timings.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
         k = len(starts)
         return [[WindowResult(st / self.sr, rows[i * k + j]) for j, st in enumerate(starts)] for i in range(self.S)]
+
+
+class PendingPush:
+    """The windows of one StreamBank.push_submit, in flight on the GPU; collect() returns push()'s result."""
+
+    __slots__ = ("pend", "starts", "S", "sr")
+
+    def __init__(self, pend, starts, S: int, sr: int):
+        self.pend, self.starts, self.S, self.sr = pend, starts, S, sr
+
+    def collect(self) -> list[list[WindowResult]]:
+        if self.pend is None:
+            return [[] for _ in range(self.S)]
+        rows = self.pend.collect()
+        k = len(self.starts)
+        return [[WindowResult(st / self.sr, rows[i * k + j]) for j, st in enumerate(self.starts)] for i in range(self.S)]

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -2385,6 +2386,141 @@ int aid_query_pcm(aid_engine *e, const float *pcm, const int64_t *offsets, int32
     if (int rc = ensure_index(e)) return rc;
     if (int rc = extract_locked(e, pcm, offsets, n_clips, loc, stream)) return drain_host_copy(e, loc, stream, rc);
     return drain_host_copy(e, loc, stream, query_extracted_locked(e, rows, nrows));
+}
+
+// ---- asynchronous windowed query: submit enqueues the extraction, K5's LDS path and the result
+// copies and returns; collect waits for the ticket's event. The ticket owns page-locked result buffers and a device copy
+// of its records (the next submit reuses the engine's extraction buffers in stream order), so a query the LDS path
+// hands back can still be answered on the global path at collect time.
+struct aid_query_ticket {
+    int nq = 0;
+    int64_t nrec = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    HostBuf<int32_t> rows, nrows;
+    HostBuf<int64_t> meta;  // [0, nq) record starts, [nq, 2nq) record counts, [2nq, 3nq) exact votes
+    DevBuf<uint64_t> recs;
+    DevBuf<int64_t> qsc;    // device record starts and counts of the ticket's queries ([0, nq), [nq, 2nq))
+    ~aid_query_ticket() {
+        if (ev) (void)hipEventDestroy(ev);
+        rows.release();
+        nrows.release();
+        meta.release();
+        recs.release();
+        qsc.release();
+    }
+};
+
+extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends,
+                                        int32_t n_windows, void *stream, aid_query_ticket **out) {
+    if (!e || n_windows < 0 || !out || (n_windows > 0 && (!starts || !ends || !pcm)))
+        return fail(AID_ERR_INVALID, "aid_query_windows_submit: bad argument");
+    *out = nullptr;
+    for (int c = 0; c < n_windows; ++c)
+        if (starts[c] < 0 || ends[c] < starts[c]) return fail(AID_ERR_INVALID, "aid_query_windows_submit: bad window");
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::unique_ptr<aid_query_ticket> t(new aid_query_ticket());
+    t->nq = n_windows;
+    HIP_TRY(hipSetDevice(e->device));
+    if (int rc = ensure_index(e)) return rc;
+    if (n_windows > 0) {
+        if (int rc = extract_locked(e, pcm, starts, n_windows, AID_PCM_DEVICE, stream, ends)) return rc;
+        if (int rc = check_query_frames(e)) return rc;
+        hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
+        t->s = s;
+        const int nq = n_windows, mr = e->cfg.max_results;
+        t->nrec = e->clip_base[nq - 1] + hash_capacity(e->clip_frames[nq - 1]);
+        HIP_TRY(t->meta.reserve((size_t)3 * nq));
+        HIP_TRY(t->rows.reserve((size_t)nq * mr * 5));
+        HIP_TRY(t->nrows.reserve((size_t)nq));
+        HIP_TRY(t->recs.reserve((size_t)std::max<int64_t>(t->nrec, 1)));
+        HIP_TRY(t->qsc.reserve((size_t)2 * nq));
+        std::memcpy(t->meta.p, e->clip_base.data(), (size_t)nq * sizeof(int64_t));
+        // the ticket's own copies: record starts (from its page-locked meta), counts and records (device to device)
+        HIP_TRY(hipMemcpyAsync(t->qsc.p, t->meta.p, (size_t)nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(t->qsc.p + nq, e->counts.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipMemcpyAsync(t->recs.p, e->records.p, (size_t)t->nrec * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipMemcpyAsync(t->meta.p + nq, e->counts.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(e->q_votes.reserve((size_t)nq));
+        HIP_TRY(e->q_ranges.reserve((size_t)std::max<int64_t>(t->nrec, 1)));
+        HIP_TRY(e->q_rows.reserve((size_t)nq * mr * 5));
+        HIP_TRY(e->q_nrows.reserve((size_t)nq));
+        launch_query_votes(t->recs.p, t->qsc.p, t->qsc.p + nq, nq, e->idx_off.p, e->q_votes.p, e->q_ranges.p, s);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(t->meta.p + 2 * nq, e->q_votes.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        {
+            ProfScope ps(e, AID_K_MATCH, s, true);
+            launch_match_lds(t->recs.p, t->qsc.p, t->qsc.p + nq, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
+                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
+                             e->idx_sig.p, e->q_ranges.p, s);
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(t->rows.p, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(t->nrows.p, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(t->ev, s));
+    }
+    *out = t.release();
+    return AID_OK;
+}
+
+extern "C" int aid_query_windows_collect(aid_engine *e, aid_query_ticket *t, aid_match_row *rows, int32_t *nrows) {
+    if (!e || !t || (t->nq > 0 && (!rows || !nrows))) {
+        delete t;
+        return fail(AID_ERR_INVALID, "aid_query_windows_collect: bad argument");
+    }
+    std::unique_ptr<aid_query_ticket> own(t);
+    if (t->nq == 0) return AID_OK;
+    HIP_TRY(hipEventSynchronize(t->ev));
+    std::lock_guard<std::mutex> lk(e->mu);
+    const int nq = t->nq, mr = e->cfg.max_results;
+    std::memcpy(rows, t->rows.p, (size_t)nq * mr * sizeof(aid_match_row));
+    const int64_t *starts = t->meta.p, *counts = starts + nq, *votes = counts + nq;
+    std::vector<int> again;
+    int n_light = 0;
+    for (int q = 0; q < nq; ++q) {
+        const int32_t n = t->nrows.p[q];
+        if (n < 0) {
+            again.push_back(q);
+            ++e->st_fb_reason[std::min(-n, 5) - 1];
+        } else {
+            nrows[q] = n;
+        }
+        e->st_votes += votes[q];
+        e->st_records += counts[q];
+        e->st_sig_reads += votes[q] <= kLdsMaxVotes ? 2 * votes[q] : 0;
+        n_light += votes[q] <= kLdsMaxVotes;
+    }
+    e->st_queries += nq;
+    e->st_q_lds += n_light;
+    e->n_fallback += (int64_t)again.size();
+    if (again.empty()) return AID_OK;
+    // the queries the LDS path handed back: the global path over the ticket's own copy of their records
+    HIP_TRY(hipSetDevice(e->device));
+    const int na = (int)again.size();
+    std::vector<int64_t> sc(2 * (size_t)na);
+    for (int i = 0; i < na; ++i) {
+        sc[i] = starts[again[i]];
+        sc[na + i] = counts[again[i]];
+    }
+    HIP_TRY(t->qsc.reserve((size_t)2 * nq));
+    HIP_TRY(hipMemcpyAsync(t->qsc.p, sc.data(), sc.size() * sizeof(int64_t), hipMemcpyHostToDevice, t->s));
+    std::vector<aid_match_row> sub((size_t)na * mr);
+    std::vector<int32_t> subn(na, 0);
+    const int keep_path = e->k5_path;
+    const int64_t q0 = e->st_queries, v0 = e->st_votes, r0 = e->st_records;
+    e->k5_path = 2;
+    const int rc = run_queries(e, t->recs.p, t->qsc.p, t->qsc.p + na, na, t->nrec, sub.data(), subn.data(), t->s);
+    e->k5_path = keep_path;
+    e->st_queries = q0;  // counted above already
+    e->st_votes = v0;
+    e->st_records = r0;
+    if (rc) return rc;
+    for (int i = 0; i < na; ++i) {
+        nrows[again[i]] = subn[i];
+        std::memcpy(rows + (size_t)again[i] * mr, sub.data() + (size_t)i * mr, (size_t)mr * sizeof(aid_match_row));
+    }
+    return AID_OK;
 }
 
 int aid_query_windows(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends, int32_t n_windows,

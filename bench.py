@@ -832,35 +832,58 @@ def stream_leg(args, rank, world, dist, torch) -> dict:
         seg_tracks, stereo = _agreed(build, "stream (index + streams)", dist)
         total_n = stereo.shape[1]
 
-        def run(n_streams, measure: bool):
+        def run(n_streams, measure: bool, pipelined: bool = False):
             bank = StreamBank(eng, n_streams, stream_sr=QSR)
             bank.timings = []
             eng.match_stats(reset=True)
             lat, res = [], [[] for _ in range(n_streams)]
+            pending = None
+
+            def take(r):
+                for i in range(n_streams):
+                    res[i] += r[i]
+
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for a in range(0, total_n, chunk):
                 t = time.perf_counter()
-                r = bank.push(stereo[:n_streams, a:a + chunk])
+                if pipelined:  # submit push N + 1, then collect push N: one push's host work beside the other's kernels
+                    p = bank.push_submit(stereo[:n_streams, a:a + chunk])
+                    if pending is not None:
+                        take(pending.collect())
+                    pending = p
+                else:
+                    take(bank.push(stereo[:n_streams, a:a + chunk]))
                 lat.append(time.perf_counter() - t)
-                for i in range(n_streams):
-                    res[i] += r[i]
+            if pending is not None:
+                take(pending.collect())
             torch.cuda.synchronize()
             return time.perf_counter() - t0, lat, res, bank.timings, eng.match_stats(reset=True)
 
         def local():
             run(S, False)  # warm-up: first-use allocations of the bank and the engine's scratch
+            run(S, False, True)
             # a serving process moves its start-up objects out of the cyclic collector's reach (gc.freeze), as a
             # long-running server does after start-up: a full collection over this process's ~10^6 objects (torch, the
             # legs before) otherwise lands inside some push (a 70 ms push in r05j, all of it outside the engine calls)
             gc.collect()
             gc.freeze()
             try:
-                return run(S, True)
+                return run(S, True), run(S, True, True)
             finally:
                 gc.unfreeze()
 
-        wall, lat, res, tim, mst = _agreed(local, "stream (pushes)", dist)
+        (wall, lat, res, tim, mst), (wall_p, lat_p, res_p, _, _) = _agreed(local, "stream (pushes)", dist)
+        wall_p_max = _max_over_ranks(wall_p, dist, torch)
+        same = all(len(a) == len(b) and all(x.start_s == y.start_s and np.array_equal(x.rows, y.rows)
+                                            for x, y in zip(a, b)) for a, b in zip(res, res_p))
+        lat_p_ms = 1e3 * np.array(lat_p)
+        out["pipelined"] = {
+            "value": round(world * S * total_n / QSR / wall_p_max, 1), "unit": "stream-audio-s/s",
+            "push_call_ms": {f"p{q}": round(float(np.percentile(lat_p_ms, q)), 3) for q in (50, 95, 99)},
+            "rows_equal_sync": bool(same),
+            "note": "StreamBank.push_submit: each iteration submits push N + 1 (aid_query_windows_submit) and then "
+                    "collects push N; a push's windows come back one push later, bit for bit those of push()"}
         worst = int(np.argmax(lat))
         out["slowest_push"] = {"index": worst, "ms": round(1e3 * lat[worst], 3),
                                "append_resample_windows_ms": [round(1e3 * x, 3) for x in tim[worst]]}
@@ -1290,6 +1313,8 @@ def main() -> int:
         if (cat.get("shard_parity") or {}).get("bit_exact") is False:
             return False
         if ((legs["stream"] or {}).get("parity") or {}).get("bit_exact") is False:
+            return False
+        if ((legs["stream"] or {}).get("pipelined") or {}).get("rows_equal_sync") is False:
             return False
         lp = (cat.get("exact_lane") or {}).get("parity")
         if not lp:

@@ -148,3 +148,72 @@ def test_stream_bank_equals_oracle_route():
         par = bench.stream_parity(eng, stereo, seg_tracks, res, 4, torch, max_windows=8)
     assert par["windows"] == 4 * 8
     assert par["bit_exact"], par
+
+
+def test_stream_bank_pipelined_equals_sync():
+    """StreamBank.push_submit (aid_query_windows_submit / _collect): submitting push N + 1 before
+    collecting push N gives every push exactly the rows of the synchronous push()."""
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.stream import StreamBank
+
+    SSR, QSR = 16000, 48000
+    with Engine(SSR) as eng:
+        ingest_synthetic(eng, np.arange(40, dtype=np.uint32), 30.0, batch=64, source_sr=44100, local=True)
+        eng.index_finalize()
+        S, seg = 5, 14 * QSR
+        tr = np.random.default_rng(9).integers(0, 40, S).astype(np.uint32)
+        stereo = torch.empty(S, seg, 2, dtype=torch.float32, device="cuda")
+        tmp = torch.empty(S * seg, dtype=torch.float32, device="cuda")
+        for ch in range(2):
+            eng.synth(tmp.data_ptr(), tr, np.zeros(S, np.int64), seg, noise_a=synth.noise_halfwidth(30.0),
+                      salt=21 + ch, sample_rate=QSR)
+            stereo[:, :, ch] = tmp.view(S, seg)
+        chunk = int(1.7 * QSR)
+        sync_bank, pipe_bank = StreamBank(eng, S, stream_sr=QSR), StreamBank(eng, S, stream_sr=QSR)
+        want, got, pending = [], [], None
+        for a in range(0, seg, chunk):
+            want.append(sync_bank.push(stereo[:, a:a + chunk]))
+            p = pipe_bank.push_submit(stereo[:, a:a + chunk])
+            if pending is not None:
+                got.append(pending.collect())
+            pending = p
+        got.append(pending.collect())
+        assert sum(len(w) for push in want for w in push) > 0
+        for w, g in zip(want, got):
+            for ws, gs in zip(w, g):
+                assert [x.start_s for x in ws] == [x.start_s for x in gs]
+                for x, y in zip(ws, gs):
+                    assert np.array_equal(x.rows, y.rows)
+
+
+def test_query_windows_submit_collect_with_fallbacks():
+    """Two tickets in flight, collected out of order, and queries the fast match path hands back (min_match 1: more
+    candidate tracks than its row staging holds): rows equal aid_query_windows' (which takes the global path for them
+    too) and the oracle's."""
+    import oracle as O
+    from aidfp.catalog import ingest_synthetic
+
+    SSR = 16000
+    with Engine(SSR, min_match=1) as eng:
+        ingest_synthetic(eng, np.arange(300, dtype=np.uint32), 30.0, batch=64, source_sr=44100, local=True)
+        eng.index_finalize()
+        n = 20 * SSR
+        pcm = torch.empty(4 * n, dtype=torch.float32, device="cuda")
+        eng.synth(pcm.data_ptr(), np.array([3, 77, 150, 299], np.uint32), np.zeros(4, np.int64), n,
+                  noise_a=synth.noise_halfwidth(20.0), salt=5, sample_rate=SSR)
+        st = np.array([0, 7 * SSR, n + 3 * SSR, 2 * n + 11, 3 * n + 5 * SSR], np.int64)
+        en = st + np.array([5, 5, 5, 9, 5], np.int64) * SSR
+        eng.match_stats(reset=True)
+        want = eng.query_windows(pcm.data_ptr(), st, en)
+        a = eng.query_windows_submit(pcm.data_ptr(), st[:3], en[:3])
+        b = eng.query_windows_submit(pcm.data_ptr(), st[3:], en[3:])
+        gb, ga = b.collect(), a.collect()
+        ms = eng.match_stats()
+        assert ms["fallback_rows"] > 0  # the case under test: some queries went to the global path
+        for w, g in zip(want, ga + gb):
+            assert np.array_equal(w, g)
+        post = eng.index_export()
+        host = pcm.cpu().numpy()
+        for k in range(len(st)):
+            rec = O.fingerprint(host[st[k]:en[k]], 256)
+            assert np.array_equal(want[k], O.query(post, rec, min_match=1, max_rows=eng.max_results))
