@@ -226,7 +226,9 @@ class StreamBank:
             self.raw_filled = keep
         dst = self.raw[:, 2 * self.raw_filled: 2 * (self.raw_filled + n)]
         if isinstance(chunk, torch.Tensor):
-            dst.copy_(chunk.reshape(self.S, 2 * n), non_blocking=True)
+            # one strided copy: a [S, n, 2] slice of a longer stream tensor is not contiguous, and reshape() had made
+            # a contiguous temporary first (a second 245 MB pass per 256-stream push, ~42 us of GPU time)
+            dst.view(self.S, n, 2).copy_(chunk, non_blocking=True)
         else:  # host chunk: through a page-locked staging buffer (an async DMA); synced before its next refill
             x = np.ascontiguousarray(chunk, dtype=np.float32).reshape(self.S, 2 * n)
             if self._pin is None or self._pin.numel() < x.size:
