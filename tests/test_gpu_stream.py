@@ -209,7 +209,9 @@ def test_query_windows_submit_collect_with_fallbacks():
         b = eng.query_windows_submit(pcm.data_ptr(), st[3:], en[3:])
         gb, ga = b.collect(), a.collect()
         ms = eng.match_stats()
-        assert ms["fallback_rows"] > 0  # the case under test: some queries went to the global path
+        # the case under test: the LDS path handed some queries back (every bucket is hot at min_match 1, so its
+        # tables fill) and collect answered them on the global path
+        assert sum(ms[k] for k in ("fallback_table", "fallback_distinct", "fallback_tracks", "fallback_rows")) > 0, ms
         for w, g in zip(want, ga + gb):
             assert np.array_equal(w, g)
         post = eng.index_export()
