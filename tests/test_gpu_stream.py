@@ -195,7 +195,7 @@ def test_query_windows_submit_collect_with_fallbacks():
 
     SSR = 16000
     with Engine(SSR, min_match=1) as eng:
-        ingest_synthetic(eng, np.arange(300, dtype=np.uint32), 30.0, batch=64, source_sr=44100, local=True)
+        ingest_synthetic(eng, np.arange(1200, dtype=np.uint32), 30.0, batch=256, source_sr=44100, local=True)
         eng.index_finalize()
         n = 20 * SSR
         pcm = torch.empty(4 * n, dtype=torch.float32, device="cuda")
