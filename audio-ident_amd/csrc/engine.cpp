@@ -170,6 +170,9 @@ struct ProfEvent {
 
 }  // namespace
 
+struct aid_engine;
+static void free_ticket_pool(aid_engine *e);
+
 struct aid_engine {
     aid_config cfg{};
     int device = 0;
@@ -237,6 +240,7 @@ struct aid_engine {
     HostBuf<int32_t> hq_n;      // run_queries: the LDS path's per-query row counts
     HostBuf<int32_t> hq_rows;   // run_queries: the LDS path's rows, [nq][max_results][5]
     HostBuf<int64_t> hq_start;  // the queries' record starts (clip_base) staged page-locked for their upload
+    std::vector<aid_query_ticket *> ticket_pool;  // collected tickets, reused: their buffers and event stay allocated
     DevBuf<int64_t> q_votes;  // exact votes per query (LDS-histogram eligibility)
     DevBuf<int64_t> x_src, x_dst;
     // batched exact lane (aid_exact_lane): PCM staging, window descriptors, consensus output
@@ -519,6 +523,7 @@ void aid_engine_destroy(aid_engine *e) {
     e->hq_n.release();
     e->hq_rows.release();
     e->hq_start.release();
+    free_ticket_pool(e);
     e->q_rows.release();
     e->q_nrows.release();
     e->x_src.release();
@@ -2411,6 +2416,11 @@ struct aid_query_ticket {
     }
 };
 
+static void free_ticket_pool(aid_engine *e) {
+    for (aid_query_ticket *t : e->ticket_pool) delete t;
+    e->ticket_pool.clear();
+}
+
 extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends,
                                         int32_t n_windows, void *stream, aid_query_ticket **out) {
     if (!e || n_windows < 0 || !out || (n_windows > 0 && (!starts || !ends || !pcm)))
@@ -2419,8 +2429,17 @@ extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const i
     for (int c = 0; c < n_windows; ++c)
         if (starts[c] < 0 || ends[c] < starts[c]) return fail(AID_ERR_INVALID, "aid_query_windows_submit: bad window");
     std::lock_guard<std::mutex> lk(e->mu);
-    std::unique_ptr<aid_query_ticket> t(new aid_query_ticket());
+    // a pooled ticket keeps its page-locked and device buffers and its event: allocating them per call (hipHostMalloc,
+    // hipMalloc, and the hipFree that synchronises the device on release) had cost more than the overlap gained
+    std::unique_ptr<aid_query_ticket> t;
+    if (!e->ticket_pool.empty()) {
+        t.reset(e->ticket_pool.back());
+        e->ticket_pool.pop_back();
+    } else {
+        t.reset(new aid_query_ticket());
+    }
     t->nq = n_windows;
+    t->nrec = 0;
     HIP_TRY(hipSetDevice(e->device));
     if (int rc = ensure_index(e)) return rc;
     if (n_windows > 0) {
@@ -2457,7 +2476,7 @@ extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const i
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(t->rows.p, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(t->nrows.p, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
+        if (!t->ev) HIP_TRY(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(t->ev, s));
     }
     *out = t.release();
@@ -2465,14 +2484,30 @@ extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const i
 }
 
 extern "C" int aid_query_windows_collect(aid_engine *e, aid_query_ticket *t, aid_match_row *rows, int32_t *nrows) {
-    if (!e || !t || (t->nq > 0 && (!rows || !nrows))) {
+    if (!e || !t) {
         delete t;
         return fail(AID_ERR_INVALID, "aid_query_windows_collect: bad argument");
     }
-    std::unique_ptr<aid_query_ticket> own(t);
-    if (t->nq == 0) return AID_OK;
-    HIP_TRY(hipEventSynchronize(t->ev));
+    if (t->nq > 0 && (!rows || !nrows)) {
+        if (t->ev) (void)hipEventSynchronize(t->ev);
+        std::lock_guard<std::mutex> lk(e->mu);
+        e->ticket_pool.push_back(t);
+        return fail(AID_ERR_INVALID, "aid_query_windows_collect: bad argument");
+    }
+    if (t->nq > 0) {
+        const hipError_t we = hipEventSynchronize(t->ev);
+        if (we != hipSuccess) {
+            delete t;
+            return fail(AID_ERR_DEVICE, std::string("aid_query_windows_collect: ") + hipGetErrorString(we));
+        }
+    }
     std::lock_guard<std::mutex> lk(e->mu);
+    struct Back {  // back to the pool on every return below (the ticket's work has completed)
+        aid_engine *e;
+        aid_query_ticket *t;
+        ~Back() { e->ticket_pool.push_back(t); }
+    } back{e, t};
+    if (t->nq == 0) return AID_OK;
     const int nq = t->nq, mr = e->cfg.max_results;
     std::memcpy(rows, t->rows.p, (size_t)nq * mr * sizeof(aid_match_row));
     const int64_t *starts = t->meta.p, *counts = starts + nq, *votes = counts + nq;
