@@ -130,6 +130,7 @@ SIGNATURES = [
     ("aid_query_windows", ctypes.c_int, [P, P, P, P, I32, P, P, P]),
     ("aid_query_windows_submit", ctypes.c_int, [P, P, P, P, I32, P, P]),
     ("aid_query_windows_collect", ctypes.c_int, [P, P, P, P]),
+    ("aid_query_pcm_submit", ctypes.c_int, [P, P, P, I32, I32, P, P]),
     ("aid_exact_lane", ctypes.c_int, [P, P, P, I32, I32, I32, P, P, P]),
     ("aid_exact_windows", ctypes.c_int, [I64, I32, P, P, P]),
     ("aid_downmix", ctypes.c_int, [P, P, I64, P, P]),

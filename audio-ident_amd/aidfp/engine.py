@@ -157,21 +157,29 @@ def _concat_into(arrs: list[np.ndarray], out: np.ndarray) -> None:
         f.result()
 
 
-def _host_concat(arrs: list[np.ndarray], total: int) -> np.ndarray:
+def _new_slot() -> _PinnedSlot:
+    sl = _PinnedSlot()
+    _pinned_slots.add(sl)
+    return sl
+
+
+def _host_concat(arrs: list[np.ndarray], total: int, slot: "_PinnedSlot | None" = None) -> np.ndarray:
     """The clips concatenated into one host array for AID_PCM_HOST. Up to _PINNED_MAX samples it is a page-locked
-    buffer of the calling thread (grown on demand), so the engine's single H2D copy of the span runs as a DMA
-    instead of through the runtime's pageable staging (coalesced service queries); the engine call has finished
-    with it when it returns (every host-PCM entry point syncs before returning its results)."""
+    buffer (grown on demand), so the engine's single H2D copy of the span runs as a DMA instead of through the
+    runtime's pageable staging (coalesced service queries). By default the calling thread's buffer: the engine call
+    has finished with it when it returns (every synchronous host-PCM entry point syncs before returning its results);
+    a submitted query passes its own `slot`, held until it is collected."""
     if total == 0:
         return np.zeros(1, dtype=np.float32)
     if total <= _PINNED_MAX:
         try:
             import torch
 
-            sl = getattr(_pinned, "slot", None)
+            sl = slot
             if sl is None:
-                sl = _pinned.slot = _PinnedSlot()
-                _pinned_slots.add(sl)
+                sl = getattr(_pinned, "slot", None)
+                if sl is None:
+                    sl = _pinned.slot = _new_slot()
             buf = sl.buf
             if buf is None or buf.numel() < total:
                 if _finalizing():
@@ -219,6 +227,8 @@ class Engine:
         self.min_match = out.min_match
         self.max_results = out.max_results
         self.n_clips = 0
+        self._free_slots: list[_PinnedSlot] = []  # page-locked PCM buffers of collected submitted queries
+        self._slot_lock = threading.Lock()
         _live.add(self)
 
     # -- lifecycle --
@@ -563,6 +573,33 @@ class Engine:
         self.n_clips = nq
         return self._rows(rows, nrows, nq)
 
+    def query_pcm_submit(self, clips: Sequence[np.ndarray]) -> "PendingQuery":
+        """query_pcm in two halves (aid_query_pcm_submit): the batch is laid into a page-locked buffer of its own,
+        its copy, extraction, K5 and result copies are queued, and a PendingQuery is returned at once; collect()
+        waits and returns the rows (the buffer is reused after that). A caller submits batch N + 1 before it
+        collects batch N (QueryCoalescer's pipelined dispatch)."""
+        arrs = [np.ascontiguousarray(c, dtype=np.float32).ravel() for c in clips]
+        nq = len(arrs)
+        offsets = np.zeros(nq + 1, dtype=np.int64)
+        if nq:
+            offsets[1:] = np.cumsum([len(a) for a in arrs])
+        with self._slot_lock:
+            slot = self._free_slots.pop() if self._free_slots else _new_slot()
+        try:
+            pcm = _host_concat(arrs, int(offsets[-1]), slot)
+            t = ctypes.c_void_p()
+            check(self._lib.aid_query_pcm_submit(self._h, _p(pcm), _p(offsets), nq, AID_PCM_HOST, None,
+                                                 ctypes.byref(t)))
+        except BaseException:
+            self._put_slot(slot)  # a failed submit has drained its copy (drain_host_copy)
+            raise
+        return PendingQuery(self, t, nq, slot, pcm)
+
+    def _put_slot(self, slot) -> None:
+        with self._slot_lock:
+            if len(self._free_slots) < 4:
+                self._free_slots.append(slot)
+
     def query_windows(self, pcm_ptr: int, starts, ends, stream: int | None = None) -> list[np.ndarray]:
         """Extract + match device-PCM windows [starts[c], ends[c]) (may overlap) in one engine call."""
         st = np.ascontiguousarray(starts, dtype=np.int64)
@@ -665,12 +702,13 @@ __all__ = ["Engine", "EngineError", "EngineUnavailable", "peaks_from_mask"]
 
 
 class PendingQuery:
-    """A submitted aid_query_windows_submit ticket; collect() once (a dropped one is collected and discarded)."""
+    """A submitted aid_query_windows_submit / aid_query_pcm_submit ticket; collect() once (a dropped one is collected
+    and discarded). A host-PCM ticket holds its page-locked buffer (and the array over it) until collected."""
 
-    __slots__ = ("eng", "ticket", "nq")
+    __slots__ = ("eng", "ticket", "nq", "slot", "pcm")
 
-    def __init__(self, eng: "Engine", ticket: ctypes.c_void_p, nq: int):
-        self.eng, self.ticket, self.nq = eng, ticket, nq
+    def __init__(self, eng: "Engine", ticket: ctypes.c_void_p, nq: int, slot=None, pcm=None):
+        self.eng, self.ticket, self.nq, self.slot, self.pcm = eng, ticket, nq, slot, pcm
 
     def collect(self) -> list[np.ndarray]:
         if self.ticket is None:
@@ -680,7 +718,12 @@ class PendingQuery:
         mr = self.eng.max_results
         rows = (AidMatchRow * max(1, nq * mr))()
         nrows = np.zeros(max(1, nq), dtype=np.int32)
-        check(self.eng._lib.aid_query_windows_collect(self.eng._h, t, ctypes.addressof(rows), _p(nrows)))
+        try:
+            check(self.eng._lib.aid_query_windows_collect(self.eng._h, t, ctypes.addressof(rows), _p(nrows)))
+        finally:  # collect waited for the ticket's work (also on error): its PCM buffer is free again
+            slot, self.slot, self.pcm = self.slot, None, None
+            if slot is not None:
+                self.eng._put_slot(slot)
         return self.eng._rows(rows, nrows[:nq], nq) if nq else []
 
     def __del__(self):  # pragma: no cover - an abandoned ticket still frees its buffers

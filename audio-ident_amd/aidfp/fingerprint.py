@@ -101,21 +101,55 @@ def db_path() -> Path:
     return Path(os.environ.get("AIDFP_DB") or os.environ.get("OLAF_DB") or DEFAULT_DB)
 
 
+class _Answered:
+    """A coalesced batch answered at submit time (its engine submit failed and the synchronous path ran)."""
+
+    __slots__ = ("out",)
+
+    def __init__(self, out):
+        self.out = out
+
+    def collect(self):
+        return self.out
+
+
+class _PendingBatch:
+    """A coalesced batch in flight: holds the service's shared lock from submit until collect()."""
+
+    __slots__ = ("svc", "eng", "pcms", "pend")
+
+    def __init__(self, svc, eng, pcms, pend):
+        self.svc, self.eng, self.pcms, self.pend = svc, eng, pcms, pend
+
+    def collect(self):
+        from ._lib import EngineError
+
+        try:
+            try:
+                rows = self.pend.collect()
+            except EngineError as exc:
+                rows = self.svc._rows_after_failure(self.eng, self.pcms, exc)
+            return self.svc._matches(self.eng, rows)
+        finally:
+            self.svc._rw.release_read()
+
+
 class FingerprintService:
     """One GPU engine + the persisted index of the OLAF_DB directory (aidfp.store: snapshot +
     write-ahead journal, so a store or delete writes O(track) bytes, not the whole index)."""
 
     def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20,
                  coalesce_window_s: float = 0.0005, max_batch: int = 256, max_batch_bytes: int = 64 << 20,
-                 coalesce_workers: int = 1):
+                 coalesce_workers: int = 1, pipeline: bool = True, split_min: int = 16):
         self.db_dir = Path(db_dir) if db_dir is not None else db_path()
         self.device = device
         self._rw = RWLock()  # index writers exclusive, queries shared
         self._init_lock = threading.Lock()  # first-use engine creation + index load
         # a coalesced batch holds at most max_batch requests and max_batch_bytes of PCM (64 MiB = 17 min of
         # 16 kHz audio): many long uploads cannot land in one extraction
+        # pipeline: the coalescer starts batch N + 1 (aid_query_pcm_submit) before it collects batch N
         self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch, max_batch_bytes,
-                                         coalesce_workers)
+                                         coalesce_workers, self._submit_batch if pipeline else None, split_min)
         self._ckpt_retry_at = 0.0  # monotonic time before which a failed auto-checkpoint is not retried
         self._engine = None
         self._store = None
@@ -291,36 +325,69 @@ class FingerprintService:
         `olaf_c query` process (fingerprint.py:197-200). A device fault or an invalid argument does not depend
         on the batch: the whole batch gets [] at once (bisecting a sticky device fault would cost ~2n failing
         engine calls under the shared lock)."""
-        from ._lib import AID_ERR_NOMEM, AID_ERR_STATE, EngineError
+        from ._lib import EngineError
 
         try:
             return eng.query_pcm([self._pcm(p) for p in pcms])
         except EngineError as exc:
-            if len(pcms) == 1 or exc.code not in (AID_ERR_STATE, AID_ERR_NOMEM):
-                logger.error("aidfp query batch of %d failed: %s", len(pcms), exc)
-                return [np.zeros((0, 5), np.int64) for _ in pcms]
-            logger.warning("aidfp query batch of %d failed (%s); retrying in halves", len(pcms), exc)
+            return self._rows_after_failure(eng, pcms, exc)
+
+    def _rows_after_failure(self, eng, pcms: list[bytes], exc) -> list:
+        """The batch's engine call (or its pipelined submit / collect) failed with `exc`: [] for every request, or
+        the batch bisected and retried if the failure depends on the batch (see _query_rows)."""
+        from ._lib import AID_ERR_NOMEM, AID_ERR_STATE
+
+        if len(pcms) == 1 or exc.code not in (AID_ERR_STATE, AID_ERR_NOMEM):
+            logger.error("aidfp query batch of %d failed: %s", len(pcms), exc)
+            return [np.zeros((0, 5), np.int64) for _ in pcms]
+        logger.warning("aidfp query batch of %d failed (%s); retrying in halves", len(pcms), exc)
         h = len(pcms) // 2
         return self._query_rows(eng, pcms[:h]) + self._query_rows(eng, pcms[h:])
+
+    def _matches(self, eng, rows) -> list[list[OlafMatch]]:
+        """Engine rows -> OlafMatch lists (under the shared lock: the name map is the index's)."""
+        sec = eng.hop / eng.sample_rate
+        outs = []
+        for r in rows:
+            out = []
+            for count, track, d, tq0, tq1 in r.tolist():
+                name = self._names.get(int(track))
+                if name is None:
+                    continue
+                out.append(OlafMatch(int(count), tq0 * sec, tq1 * sec, name, int(track), (tq0 + d) * sec,
+                                     (tq1 + d) * sec))
+            out.sort(key=lambda m: m.match_count, reverse=True)
+            outs.append(out)
+        return outs
 
     def _query_batch(self, pcms: list[bytes]) -> list[list[OlafMatch]]:
         """One engine call for every query the coalescer gathered (under the shared lock)."""
         with self._rw.read():
             eng = self._eng()
-            rows = self._query_rows(eng, pcms)
-            sec = eng.hop / eng.sample_rate
-            outs = []
-            for r in rows:
-                out = []
-                for count, track, d, tq0, tq1 in r.tolist():
-                    name = self._names.get(int(track))
-                    if name is None:
-                        continue
-                    out.append(OlafMatch(int(count), tq0 * sec, tq1 * sec, name, int(track), (tq0 + d) * sec,
-                                         (tq1 + d) * sec))
-                out.sort(key=lambda m: m.match_count, reverse=True)
-                outs.append(out)
-            return outs
+            return self._matches(eng, self._query_rows(eng, pcms))
+
+    def _submit_batch(self, pcms: list[bytes], behind: bool):
+        """The coalescer's pipelined half: take the shared lock, queue the batch (aid_query_pcm_submit) and return
+        a handle whose collect() answers it and releases the lock. With a batch still outstanding (`behind`) the
+        lock is taken only if no writer waits for it (else None: the coalescer finishes that batch first)."""
+        from ._lib import EngineError
+
+        if behind:
+            if not self._rw.try_acquire_read():
+                return None
+        else:
+            self._rw.acquire_read()
+        try:
+            eng = self._eng()
+            try:
+                return _PendingBatch(self, eng, pcms, eng.query_pcm_submit([self._pcm(p) for p in pcms]))
+            except EngineError as exc:  # answered now (bisecting a batch-dependent failure)
+                out = self._matches(eng, self._rows_after_failure(eng, pcms, exc))
+        except BaseException:
+            self._rw.release_read()
+            raise
+        self._rw.release_read()
+        return _Answered(out)
 
     def exact_batch(self, clips: list[bytes], max_results: int) -> list[list]:
         """Batched exact lane over the engine (aid_exact_lane); ranked ScoredCandidate lists."""

@@ -270,6 +270,7 @@ struct aid_engine {
     // h_desc is the source of an async H2D copy; pcm_stage is read by K1
     hipEvent_t desc_ev = nullptr, stage_ev = nullptr;
     bool desc_ev_live = false, stage_ev_live = false;
+    hipStream_t stage_stream = nullptr;  // the stream whose K1 read pcm_stage last
     std::vector<int64_t> desc_key;  // offsets (+ pcm location) the device descriptors were built for
     ClipDesc *desc_dev_for_key = nullptr;
     std::vector<int64_t> clip_base;  // host copy of desc[c].hash_base
@@ -780,10 +781,10 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
     HIP_TRY(e->counts.reserve((size_t)n_clips + 1));
     const float *dpcm = pcm;
     if (loc == AID_PCM_HOST && staged > 0) {
-        if (e->stage_ev_live) {  // K1 of an earlier call may still read the staging buffer
-            HIP_TRY(hipEventSynchronize(e->stage_ev));
-            e->stage_ev_live = false;
-        }
+        // K1 of an earlier call may still read the staging buffer: on the same stream the new copy is ordered after
+        // it (a pipelined submit must not wait for the previous batch's K1), on another stream the host waits
+        if (e->stage_ev_live && e->stage_stream != s) HIP_TRY(hipEventSynchronize(e->stage_ev));
+        e->stage_ev_live = false;
         // one copy of the clips' whole span (clips at odd offsets are read with dword-aligned float2 loads; a copy
         // per clip cost ~10-20 us of call overhead each: 64 coalesced service queries ~1 ms)
         HIP_TRY(e->pcm_stage.reserve((size_t)staged));
@@ -827,6 +828,7 @@ static int extract_locked(aid_engine *e, const float *pcm, const int64_t *offset
                 if (!e->stage_ev) HIP_TRY(hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
                 HIP_TRY(hipEventRecord(e->stage_ev, s));
                 e->stage_ev_live = true;
+                e->stage_stream = s;
             }
             {
                 ProfScope ps(e, AID_K_PEAKS, s, true);
@@ -2421,6 +2423,62 @@ static void free_ticket_pool(aid_engine *e) {
     e->ticket_pool.clear();
 }
 
+static aid_query_ticket *take_ticket(aid_engine *e) {
+    // a pooled ticket keeps its page-locked and device buffers and its event: allocating them per call (hipHostMalloc,
+    // hipMalloc, and the hipFree that synchronises the device on release) had cost more than the overlap gained
+    if (e->ticket_pool.empty()) return new aid_query_ticket();
+    aid_query_ticket *t = e->ticket_pool.back();
+    e->ticket_pool.pop_back();
+    return t;
+}
+
+// the body both submit entries share (engine lock held): the extraction of n clips, K5's LDS pass over the ticket's
+// own copy of the records, the result copies into its page-locked buffers and its event
+static int submit_locked(aid_engine *e, const float *pcm, const int64_t *offsets, const int64_t *ends, int32_t n,
+                         int32_t loc, void *stream, aid_query_ticket *t) {
+    t->nq = n;
+    t->nrec = 0;
+    HIP_TRY(hipSetDevice(e->device));
+    if (int rc = ensure_index(e)) return rc;
+    if (n == 0) return AID_OK;
+    if (int rc = extract_locked(e, pcm, offsets, n, loc, stream, ends)) return rc;
+    if (int rc = check_query_frames(e)) return rc;
+    hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
+    t->s = s;
+    const int nq = n, mr = e->cfg.max_results;
+    t->nrec = e->clip_base[nq - 1] + hash_capacity(e->clip_frames[nq - 1]);
+    HIP_TRY(t->meta.reserve((size_t)3 * nq));
+    HIP_TRY(t->rows.reserve((size_t)nq * mr * 5));
+    HIP_TRY(t->nrows.reserve((size_t)nq));
+    HIP_TRY(t->recs.reserve((size_t)std::max<int64_t>(t->nrec, 1)));
+    HIP_TRY(t->qsc.reserve((size_t)2 * nq));
+    std::memcpy(t->meta.p, e->clip_base.data(), (size_t)nq * sizeof(int64_t));
+    // the ticket's own copies: record starts (from its page-locked meta), counts and records (device to device)
+    HIP_TRY(hipMemcpyAsync(t->qsc.p, t->meta.p, (size_t)nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(t->qsc.p + nq, e->counts.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(t->recs.p, e->records.p, (size_t)t->nrec * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(t->meta.p + nq, e->counts.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(e->q_votes.reserve((size_t)nq));
+    HIP_TRY(e->q_ranges.reserve((size_t)std::max<int64_t>(t->nrec, 1)));
+    HIP_TRY(e->q_rows.reserve((size_t)nq * mr * 5));
+    HIP_TRY(e->q_nrows.reserve((size_t)nq));
+    launch_query_votes(t->recs.p, t->qsc.p, t->qsc.p + nq, nq, e->idx_off.p, e->q_votes.p, e->q_ranges.p, s);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(t->meta.p + 2 * nq, e->q_votes.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    {
+        ProfScope ps(e, AID_K_MATCH, s, true);
+        launch_match_lds(t->recs.p, t->qsc.p, t->qsc.p + nq, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
+                         e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
+                         e->idx_sig.p, e->q_ranges.p, s);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(t->rows.p, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(t->nrows.p, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (!t->ev) HIP_TRY(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(t->ev, s));
+    return AID_OK;
+}
+
 extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends,
                                         int32_t n_windows, void *stream, aid_query_ticket **out) {
     if (!e || n_windows < 0 || !out || (n_windows > 0 && (!starts || !ends || !pcm)))
@@ -2429,56 +2487,29 @@ extern "C" int aid_query_windows_submit(aid_engine *e, const float *pcm, const i
     for (int c = 0; c < n_windows; ++c)
         if (starts[c] < 0 || ends[c] < starts[c]) return fail(AID_ERR_INVALID, "aid_query_windows_submit: bad window");
     std::lock_guard<std::mutex> lk(e->mu);
-    // a pooled ticket keeps its page-locked and device buffers and its event: allocating them per call (hipHostMalloc,
-    // hipMalloc, and the hipFree that synchronises the device on release) had cost more than the overlap gained
-    std::unique_ptr<aid_query_ticket> t;
-    if (!e->ticket_pool.empty()) {
-        t.reset(e->ticket_pool.back());
-        e->ticket_pool.pop_back();
-    } else {
-        t.reset(new aid_query_ticket());
-    }
-    t->nq = n_windows;
-    t->nrec = 0;
-    HIP_TRY(hipSetDevice(e->device));
-    if (int rc = ensure_index(e)) return rc;
-    if (n_windows > 0) {
-        if (int rc = extract_locked(e, pcm, starts, n_windows, AID_PCM_DEVICE, stream, ends)) return rc;
-        if (int rc = check_query_frames(e)) return rc;
-        hipStream_t s = e->last_stream ? e->last_stream : e->own_stream;
-        t->s = s;
-        const int nq = n_windows, mr = e->cfg.max_results;
-        t->nrec = e->clip_base[nq - 1] + hash_capacity(e->clip_frames[nq - 1]);
-        HIP_TRY(t->meta.reserve((size_t)3 * nq));
-        HIP_TRY(t->rows.reserve((size_t)nq * mr * 5));
-        HIP_TRY(t->nrows.reserve((size_t)nq));
-        HIP_TRY(t->recs.reserve((size_t)std::max<int64_t>(t->nrec, 1)));
-        HIP_TRY(t->qsc.reserve((size_t)2 * nq));
-        std::memcpy(t->meta.p, e->clip_base.data(), (size_t)nq * sizeof(int64_t));
-        // the ticket's own copies: record starts (from its page-locked meta), counts and records (device to device)
-        HIP_TRY(hipMemcpyAsync(t->qsc.p, t->meta.p, (size_t)nq * sizeof(int64_t), hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(t->qsc.p + nq, e->counts.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-        HIP_TRY(hipMemcpyAsync(t->recs.p, e->records.p, (size_t)t->nrec * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-        HIP_TRY(hipMemcpyAsync(t->meta.p + nq, e->counts.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIP_TRY(e->q_votes.reserve((size_t)nq));
-        HIP_TRY(e->q_ranges.reserve((size_t)std::max<int64_t>(t->nrec, 1)));
-        HIP_TRY(e->q_rows.reserve((size_t)nq * mr * 5));
-        HIP_TRY(e->q_nrows.reserve((size_t)nq));
-        launch_query_votes(t->recs.p, t->qsc.p, t->qsc.p + nq, nq, e->idx_off.p, e->q_votes.p, e->q_ranges.p, s);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(t->meta.p + 2 * nq, e->q_votes.p, (size_t)nq * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        {
-            ProfScope ps(e, AID_K_MATCH, s, true);
-            launch_match_lds(t->recs.p, t->qsc.p, t->qsc.p + nq, nq, e->idx_off.p, e->idx_post.p, e->tomb.p, e->n_tracks,
-                             e->cfg.min_match, mr, e->q_rows.p, e->q_nrows.p, e->tomb_since_build > 0, e->q_votes.p,
-                             e->idx_sig.p, e->q_ranges.p, s);
-        }
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipMemcpyAsync(t->rows.p, e->q_rows.p, (size_t)nq * mr * sizeof(aid_match_row), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(t->nrows.p, e->q_nrows.p, (size_t)nq * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        if (!t->ev) HIP_TRY(hipEventCreateWithFlags(&t->ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(t->ev, s));
-    }
+    std::unique_ptr<aid_query_ticket> t(take_ticket(e));
+    if (int rc = submit_locked(e, pcm, starts, ends, n_windows, AID_PCM_DEVICE, stream, t.get())) return rc;
+    *out = t.release();
+    return AID_OK;
+}
+
+// aid_query_pcm in two halves (the query coalescer's pipelined batches): host PCM must stay unchanged until the ticket
+// is collected (its one H2D copy is queued, not waited for)
+extern "C" int aid_query_pcm_submit(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips,
+                                    int32_t loc, void *stream, aid_query_ticket **out) {
+    if (!e || !offsets || n_clips < 0 || !out) return fail(AID_ERR_INVALID, "aid_query_pcm_submit: bad argument");
+    *out = nullptr;
+    if (loc != AID_PCM_HOST && loc != AID_PCM_DEVICE)
+        return fail(AID_ERR_INVALID, "aid_query_pcm_submit: bad pcm_location");
+    if (n_clips > 0 && !pcm && offsets[n_clips] > offsets[0])
+        return fail(AID_ERR_INVALID, "aid_query_pcm_submit: null pcm");
+    for (int c = 0; c < n_clips; ++c)
+        if (offsets[c + 1] < offsets[c] || offsets[c] < 0)
+            return fail(AID_ERR_INVALID, "aid_query_pcm_submit: offsets must be non-decreasing and >= 0");
+    std::lock_guard<std::mutex> lk(e->mu);
+    std::unique_ptr<aid_query_ticket> t(take_ticket(e));
+    if (int rc = submit_locked(e, pcm, offsets, nullptr, n_clips, loc, stream, t.get()))
+        return drain_host_copy(e, loc, stream, rc);
     *out = t.release();
     return AID_OK;
 }

@@ -986,7 +986,8 @@ def service_leg(args, rank, world, dist, torch) -> dict:
     out: dict = {}
     with tempfile.TemporaryDirectory() as db:
         svc = fp.FingerprintService(Path(db), device=torch.cuda.current_device(),
-                                    coalesce_workers=args.service_workers)
+                                    coalesce_workers=args.service_workers, pipeline=bool(args.service_pipeline),
+                                    split_min=args.service_split_min)
         svc.persist = False
 
         def build():
@@ -1043,13 +1044,17 @@ def service_leg(args, rank, world, dist, torch) -> dict:
                         await asyncio.gather(*(client() for _ in range(c)))
 
                     svc._coalescer.batches.clear()
+                    svc._coalescer.overlapped = 0
                     t0 = time.perf_counter()
                     asyncio.run(level())
                     wall = time.perf_counter() - t0
                     b = np.array(svc._coalescer.batches)
                     res[str(c)] = {"requests": n_req, "qps": round(n_req / wall, 1),
                                    **{f"p{q}_ms": round(1e3 * float(np.percentile(lat, q)), 3) for q in (50, 95, 99)},
+                                   # the same without each client's first request (the level's start-up round)
+                                   "p95_ms_after_first_round": round(1e3 * float(np.percentile(lat[c:], 95)), 3),
                                    "mean_batch": round(float(b.mean()), 2) if len(b) else 0.0,
+                                   "overlapped_batches": int(svc._coalescer.overlapped),
                                    "top1": round(float(hits.mean()), 4)}
                 gc.unfreeze()
                 return res
@@ -1068,8 +1073,13 @@ def service_leg(args, rank, world, dist, torch) -> dict:
                       "eval_exact_p95_ms": 2000.0, "eval_exact_p95_ok": worst_p95 <= 2000.0,
                       "exact_lane_timeout_ms": 3000.0, "p99_within_timeout": max(v["p99_ms"] for v in res.values()) <= 3000.0,
                       "sources": "scripts/eval_exact.py:53 (p95 <= 2000 ms); app/search/orchestrator.py:31 (3 s)"}
-    out["path"] = ("aidfp.fingerprint.olaf_query -> QueryCoalescer -> aid_query_pcm (K1-K3 + K5 per coalesced batch); "
-                   "48 kHz stereo -> 16 kHz by K6 before the call, as ffmpeg in decode.py")
+    out["pipelined"] = bool(args.service_pipeline)
+    out["split_min"] = args.service_split_min if args.service_pipeline else None
+    out["path"] = ("aidfp.fingerprint.olaf_query -> QueryCoalescer -> "
+                   + ("aid_query_pcm_submit / _collect, batch N + 1 submitted before batch N is collected"
+                      if args.service_pipeline else "aid_query_pcm")
+                   + " (K1-K3 + K5 per coalesced batch); 48 kHz stereo -> 16 kHz by K6 before the call, as ffmpeg in "
+                   "decode.py")
     return out
 
 
@@ -1106,6 +1116,11 @@ def main() -> int:
     ap.add_argument("--no-service", action="store_true", help="skip the drop-in service leg")
     ap.add_argument("--service-tracks", type=int, default=10000)
     ap.add_argument("--service-workers", type=int, default=1, help="coalescer dispatcher threads of the service leg")
+    ap.add_argument("--service-pipeline", type=int, default=1, choices=(0, 1),
+                    help="1: the coalescer submits batch N + 1 before it collects batch N (aid_query_pcm_submit)")
+    ap.add_argument("--service-split-min", type=int, default=16,
+                    help="pipelined: a batch of at least this many requests gathered with none in flight runs as two "
+                         "halves (0: never split)")
     ap.add_argument("--service-requests", type=int, default=512)
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print one line per rank and exit without touching the GPU (tests)")

@@ -328,12 +328,17 @@ int aid_query_windows(aid_engine *e, const float *pcm, const int64_t *starts, co
 /* The same query in two halves (a caller overlaps its next batch's host work with this batch's
  * kernels). _submit enqueues the extraction, K5 and the result copies on `stream` and returns a ticket at once;
  * _collect waits for that ticket's work, answers any query the fast match path handed back, writes the rows exactly
- * as aid_query_windows would and frees the ticket (also on error). Tickets are collected in submit order; the
- * windows' PCM must stay unchanged until the ticket's work has run (it is read in stream order). */
+ * as aid_query_windows would and hands the ticket back to the engine's pool (also on error). Tickets may be collected
+ * in any order; the windows' PCM must stay unchanged until the ticket's work has run (it is read in stream order). */
 typedef struct aid_query_ticket aid_query_ticket;
 int aid_query_windows_submit(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends,
                              int32_t n_windows, void *stream, aid_query_ticket **ticket);
 int aid_query_windows_collect(aid_engine *e, aid_query_ticket *ticket, aid_match_row *rows, int32_t *nrows);
+/* aid_query_pcm in the same two halves (the query coalescer's pipelined batches, replacing the per-request
+ * `olaf_c query` processes of fingerprint.py:185-193): HOST PCM is copied to the device in stream order, so the
+ * caller keeps it unchanged until it has collected the ticket (with aid_query_windows_collect). */
+int aid_query_pcm_submit(aid_engine *e, const float *pcm, const int64_t *offsets, int32_t n_clips,
+                         int32_t pcm_location, void *stream, aid_query_ticket **ticket);
 
 /* Batched exact lane: replaces app/search/exact.py run_exact_lane's
    sub-window fan-out, the olaf_query calls and the consensus (exact.py:70-124, :132-353) for a

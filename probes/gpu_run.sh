@@ -10,7 +10,8 @@
 #   segv   VERDICT r5 #2: the r05y2 command (service leg under --kernel-trace --memory-copy-trace), once
 #   counters  rocprofv3 -L
 #   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/k2pf2 (probes/run_ab_lib.sh, 3 rounds)
-#   svcab  the service leg with 1 vs 2 coalescer dispatcher threads, interleaved, 2 rounds
+#   ctests the GPU tests of the service, its coalescer and the stream bank only
+#   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
 #   streamprof  probes/stream_host_profile.py (256 streams: push wall time, GPU kernels per push, cProfile)
 #   streamtrace the same probe under rocprofv3 --runtime-trace --kernel-trace (HIP API durations: host waits)
 #   k5mm   config 4 (bench_match.py, 100k tracks, 10k + 1k clips) at engine min_match 10 and 12: K5 time, fallbacks
@@ -26,6 +27,7 @@ for step in "$@"; do
   i=$((i + 1))
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 ;;
+    ctests) timeout -k 10 400 python -u -m pytest tests/test_gpu_concurrency.py tests/test_gpu_adapter.py tests/test_gpu_stream.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_ctests.txt 2>&1 ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     bench) timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err ;;
     music) timeout -k 10 900 python3 -u probes/music_eval.py --tracks 1000 --queries 500 --negatives 100 --workers 16 > $O/music.json 2> $O/music.err ;;
@@ -49,8 +51,8 @@ for step in "$@"; do
       timeout -k 10 400 python3 bench_match.py --no-cpu --category-queries 200 --min-match 12 > $O/k5mm12.json 2> $O/k5mm12.err ;;
     svcab)
       rc=0
-      for r in 1 2; do for w in 1 2; do
-        timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-workers $w > $O/svc_w${w}_r$r.json 2> $O/svc_w${w}_r$r.err || { rc=$?; break 2; }
+      for r in 1 2; do for v in "0 0" "1 0" "1 16" "1 32"; do set -- $v
+        timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-pipeline $1 --service-split-min $2 > $O/svc_p$1_s$2_r$r.json 2> $O/svc_p$1_s$2_r$r.err || { rc=$?; break 2; }
       done; done
       [ $rc -eq 0 ] ;;
     *) echo "unknown step $step"; exit 2 ;;

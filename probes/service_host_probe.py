@@ -34,6 +34,7 @@ class FakeEngine:
     def __init__(self, gpu_ms: float, rows_per_query: int):
         self.gpu_s = gpu_ms * 1e-3
         self.k = rows_per_query
+        self._slot = E._new_slot()
 
     def close(self):
         pass
@@ -43,6 +44,27 @@ class FakeEngine:
         total = sum(len(a) for a in arrs)
         E._host_concat(arrs, total)  # the real staging copy
         time.sleep(self.gpu_s)  # the engine call: GIL released (ctypes), H2D + kernels
+        return self._answer(clips)
+
+    def query_pcm_submit(self, clips):
+        """The pipelined half: the staging copy now; the 'GPU' finishes gpu_ms after the previous submit's work (one
+        stream), and collect() sleeps until then."""
+        arrs = [np.ascontiguousarray(c, dtype=np.float32).ravel() for c in clips]
+        E._host_concat(arrs, sum(len(a) for a in arrs), self._slot)
+        now = time.perf_counter()
+        self._busy_until = max(now, getattr(self, "_busy_until", 0.0)) + self.gpu_s
+        done, out = self._busy_until, self._answer(clips)
+
+        class Pending:
+            def collect(self_):
+                left = done - time.perf_counter()
+                if left > 0:
+                    time.sleep(left)
+                return out
+
+        return Pending()
+
+    def _answer(self, clips):
         out = []
         for i in range(len(clips)):
             r = np.zeros((self.k, 5), np.int64)
@@ -52,8 +74,10 @@ class FakeEngine:
         return out
 
 
-def run(workers: int, clients: int, n_req: int, gpu_ms: float, rows: int) -> dict:
-    svc = fp.FingerprintService(Path("/tmp/aidfp_probe_db"), coalesce_workers=workers)
+def run(workers: int, clients: int, n_req: int, gpu_ms: float, rows: int, pipeline: bool = False,
+        max_batch: int = 256, split_min: int = 0) -> dict:
+    svc = fp.FingerprintService(Path("/tmp/aidfp_probe_db"), coalesce_workers=workers, pipeline=pipeline,
+                                max_batch=max_batch, split_min=split_min)
     svc.persist = False
     svc._engine = FakeEngine(gpu_ms, rows)
     svc._names = {i: f"track-{i}" for i in range(1000)}
@@ -85,7 +109,8 @@ def run(workers: int, clients: int, n_req: int, gpu_ms: float, rows: int) -> dic
     b = np.array(svc._coalescer.batches)
     fp.set_service(None)
     svc.close()
-    return {"workers": workers, "clients": clients, "gpu_ms": gpu_ms, "qps": round(n_req / wall, 1),
+    return {"workers": workers, "pipeline": pipeline, "max_batch": max_batch, "split_min": split_min, "overlapped": svc._coalescer.overlapped,
+            "clients": clients, "gpu_ms": gpu_ms, "qps": round(n_req / wall, 1),
             "p50_ms": round(1e3 * float(np.percentile(lat, 50)), 3), "p95_ms": round(1e3 * float(np.percentile(lat, 95)), 3),
             "mean_batch": round(float(b.mean()), 2)}
 
@@ -97,20 +122,24 @@ def main():
     ap.add_argument("--gpu-ms", type=float, default=0.7)
     ap.add_argument("--rows", type=int, default=3)
     ap.add_argument("--workers", type=int, nargs="+", default=[1, 2])
+    ap.add_argument("--pipeline", type=int, nargs="+", default=[0], help="0/1: the coalescer's pipelined dispatch")
+    ap.add_argument("--max-batch", type=int, nargs="+", default=[256])
+    ap.add_argument("--split-min", type=int, nargs="+", default=[0])
     ap.add_argument("--profile", action="store_true")
     a = ap.parse_args()
-    for w in a.workers:
+    for w, pl, mb, sm in [(w, pl, mb, sm) for w in a.workers for pl in a.pipeline for mb in a.max_batch
+                          for sm in a.split_min]:
         if a.profile:
             import cProfile
             import pstats
 
             pr = cProfile.Profile()
             pr.enable()
-            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows)
+            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows, bool(pl), mb, sm)
             pr.disable()
             pstats.Stats(pr).sort_stats("tottime").print_stats(18)
         else:
-            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows)
+            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows, bool(pl), mb, sm)
         print(json.dumps(r), flush=True)
 
 

@@ -150,3 +150,90 @@ def test_coalescer_async_requests_resolved_per_batch():
         c.close()
     # batches: {0}, {1..32}, {bad, 5} (maybe split), {7, 8} (maybe split): far fewer callbacks than the 37 requests
     assert n <= 8, n
+
+
+class _Handle:
+    def __init__(self, log, batch, gate, fail=False):
+        self.log, self.batch, self.gate, self.fail = log, batch, gate, fail
+
+    def collect(self):
+        self.gate.wait(5)
+        self.log.append(("collect", list(self.batch)))
+        if self.fail:
+            raise ValueError("collect failed")
+        return [x * 10 for x in self.batch]
+
+
+def test_coalescer_pipelined_dispatch_overlaps_and_keeps_results():
+    """submit_batch (the service's aid_query_pcm_submit path): under load the dispatcher starts batch N + 1 before it
+    collects batch N; every request still gets its own result, FIFO, and a lone request is answered at once."""
+    log = []
+    gate = threading.Event()
+    gate.set()
+
+    def submit(batch, behind):
+        log.append(("submit", list(batch), behind))
+        return _Handle(log, batch, gate)
+
+    c = QueryCoalescer(lambda b: pytest.fail("synchronous runner used"), window_s=0.002, max_batch=8,
+                       submit_batch=submit)
+    assert c(3) == 30  # lone request: submitted and collected at once (nothing to overlap with)
+    gate.clear()
+    futs = [c.submit(i) for i in range(40)]
+    time.sleep(0.05)
+    gate.set()
+    assert [f.result(5) for f in futs] == [i * 10 for i in range(40)]
+    subs = [e for e in log if e[0] == "submit"]
+    assert [x for e in subs[1:] for x in e[1]] == list(range(40))  # FIFO
+    assert c.overlapped > 0 and any(e[2] for e in subs)
+    # the overlap: some batch is submitted before the previous one is collected
+    order = [(e[0], tuple(e[1])) for e in log]
+    assert any(order[i][0] == "submit" and order[i + 1][0] == "collect" and order[i][1] != order[i + 1][1]
+               for i in range(len(order) - 1))
+    c.close()
+
+
+def test_coalescer_pipelined_busy_and_failures():
+    """A runner that declines a batch beside the outstanding one (a writer waits for the index lock) is called again
+    once that batch is collected; a failing submit or collect fails its own batch only."""
+    log = []
+    gate = threading.Event()
+    gate.set()
+    declined = []
+
+    def submit(batch, behind):
+        if "bad-submit" in batch:
+            raise ValueError("submit failed")
+        if behind and len(declined) < 3:
+            declined.append(list(batch))
+            return None
+        log.append(("submit", list(batch), behind))
+        return _Handle(log, batch, gate, fail="bad-collect" in batch)
+
+    c = QueryCoalescer(lambda b: pytest.fail("synchronous runner used"), window_s=0.002, max_batch=4,
+                       submit_batch=submit)
+    gate.clear()
+    futs = [c.submit(i) for i in range(20)]
+    time.sleep(0.05)
+    gate.set()
+    assert [f.result(5) for f in futs] == [i * 10 for i in range(20)]
+    assert len(declined) == 3  # each declined batch ran after the outstanding one, not lost
+    for bad in ("bad-submit", "bad-collect"):
+        f = c.submit(bad)
+        with pytest.raises(ValueError):
+            f.result(5)
+        assert c(2) == 20  # the dispatcher survives
+    c.close()
+
+
+def test_rwlock_try_read():
+    lk = RWLock()
+    assert lk.try_acquire_read()
+    w = threading.Thread(target=lambda: (lk.acquire_write(), lk.release_write()))
+    w.start()
+    time.sleep(0.05)
+    assert not lk.try_acquire_read()  # a writer waits: no second hold without waiting
+    lk.release_read()
+    w.join(5)
+    assert lk.try_acquire_read()
+    lk.release_read()

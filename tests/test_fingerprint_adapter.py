@@ -65,6 +65,11 @@ class FakeEngine:
             out.append(self.query_extracted()[0])
         return out
 
+    def query_pcm_submit(self, clips):  # the coalescer's pipelined half: answered at submit, handed back at collect
+        out = self.query_pcm(clips)
+        self.submits = getattr(self, "submits", 0) + 1
+        return type("Pending", (), {"collect": lambda _self: out})()
+
     def index_save(self, path):
         blob = json.dumps({"tracks": {str(t): v.tolist() for t, v in self.tracks.items()},
                            "removed": sorted(self.removed)})
@@ -528,3 +533,21 @@ def test_register_tracks_names_a_bulk_catalog(svc, tmp_path):
     svc.checkpoint()
     again = fp.FingerprintService(tmp_path / "db")
     assert again.query(_pcm_of(0.25))[0].reference_path == "bulk-7"
+
+
+def test_pipelined_service_batches_equal_serial(svc):
+    """The service's coalescer runs its batches through the engine's submit / collect halves (pipelined dispatch):
+    concurrent olaf_query calls get exactly the rows of serial queries; pipeline=False keeps the one-call path."""
+    for i in range(4):
+        assert run(fp.olaf_index_track(_pcm_of(0.1 * (i + 1)), uuid.UUID(int=4000 + i)))
+    pcms = [_pcm_of(0.1 * (i % 5 + 1)) for i in range(24)]
+    serial = [svc.query(p) for p in pcms]
+
+    async def many():
+        return await asyncio.gather(*[fp.olaf_query(p) for p in pcms])
+
+    assert run(many()) == serial
+    assert svc._eng().submits >= 1
+    assert svc._coalescer._submit is not None
+    off = fp.FingerprintService(svc.db_dir, pipeline=False)
+    assert off._coalescer._submit is None

@@ -82,3 +82,39 @@ def test_queries_with_interleaved_writer(service):
     assert not t.is_alive() and not errors
     # track 5000's audio is not among the queries, so its brief presence changes no row
     assert conc == serial
+
+
+def test_query_pcm_submit_equals_query_pcm(service):
+    """aid_query_pcm_submit (the coalescer's pipelined half): two batches in flight at once, each with its own
+    page-locked PCM, collected out of order, give aid_query_pcm's rows bit for bit."""
+    import numpy as np
+
+    eng = service._eng()
+    qs = [np.frombuffer(q, dtype="<f4") for q in _queries(24)]
+    ref = eng.query_pcm(qs)
+    a = eng.query_pcm_submit(qs[:12])
+    b = eng.query_pcm_submit(qs[12:])
+    got = b.collect()
+    got = a.collect() + got
+    assert len(got) == 24 and all(np.array_equal(x, y) for x, y in zip(got, ref))
+    assert sum(len(r) > 0 for r in ref) >= 15
+    assert eng.query_pcm_submit([]).collect() == []
+
+
+def test_pipelined_batches_overlap_and_equal_serial(service):
+    """Small batches (max_batch 8) under 64 requests in flight: the dispatcher starts batch N + 1 before it collects
+    batch N, and every request still gets its serial rows."""
+    qs = _queries(64)
+    serial = [service.query(q) for q in qs]
+    c = service._coalescer
+    keep = c.max_batch
+    c.max_batch = 8
+    c.overlapped = 0
+    try:
+        async def fan_out():
+            return await asyncio.gather(*(fp.olaf_query(q) for q in qs))
+
+        assert asyncio.run(fan_out()) == serial
+        assert c.overlapped > 0
+    finally:
+        c.max_batch = keep
