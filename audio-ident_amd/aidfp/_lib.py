@@ -138,6 +138,7 @@ SIGNATURES = [
     ("aid_resample", ctypes.c_int, [P, P, I64, I32, I32, I32, P, I64, P, P]),
     ("aid_resample_range", ctypes.c_int, [P, P, I64, I64, I32, I32, I32, I64, I64, P, P]),
     ("aid_resample_batch", ctypes.c_int, [P, P, I64, I32, I64, I64, I32, I32, I32, I64, I64, P, I64, P]),
+    ("aid_resample_batch_split", ctypes.c_int, [P, P, I64, I64, P, I64, I32, I64, I64, I32, I32, I32, I64, I64, P, I64, P]),
     ("aid_resample_plan", ctypes.c_int, [I32, I32, P, P, P, P]),
     ("aid_dedup_reset", ctypes.c_int, [P]),
     ("aid_dedup_add", ctypes.c_int, [P, P, P, P, I32]),

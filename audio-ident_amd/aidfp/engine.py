@@ -431,6 +431,17 @@ class Engine:
                                            int(count), ctypes.c_void_p(dst_ptr), int(dst_stride),
                                            ctypes.c_void_p(stream) if stream else None))
 
+    def resample_batch_split(self, hist_ptr: int, hist_stride: int, hist_n: int, src_ptr: int, src_stride: int,
+                             n_streams: int, in_base: int, n: int, channels: int, sr_in: int, sr_out: int, m_first: int,
+                             count: int, dst_ptr: int, dst_stride: int, stream: int | None = None) -> None:
+        """resample_batch over stream frames [in_base - hist_n, in_base) at hist_ptr then [in_base, in_base + n) at
+        src_ptr (aid_resample_batch_split): a chunk is read in place, only its predecessor's tail is kept."""
+        check(self._lib.aid_resample_batch_split(self._h, ctypes.c_void_p(hist_ptr), int(hist_stride), int(hist_n),
+                                                 ctypes.c_void_p(src_ptr), int(src_stride), int(n_streams),
+                                                 int(in_base), int(n), int(channels), int(sr_in), int(sr_out),
+                                                 int(m_first), int(count), ctypes.c_void_p(dst_ptr), int(dst_stride),
+                                                 ctypes.c_void_p(stream) if stream else None))
+
     def resample_plan(self, sr_in: int, sr_out: int):
         v = [ctypes.c_int32() for _ in range(4)]
         if not self._lib.aid_resample_plan(int(sr_in), int(sr_out), *[ctypes.byref(x) for x in v]):

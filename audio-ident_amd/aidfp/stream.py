@@ -175,10 +175,11 @@ class StreamBank:
     """S live streams identified in lockstep (BASELINE config 5 at serving scale).
 
     Every push hands over the same length of interleaved stereo for every stream ([S, n, 2] float32, a device
-    tensor or a host array). Per push the whole bank costs ONE K6 launch (aid_resample_batch: downmix + polyphase
-    resampling of all S streams, each keeping its own filter history, so chunked output equals whole-signal
-    resampling bit for bit) and ONE extraction + match call over every window the push completed in every stream
-    (aid_query_windows: K1-K3 read the 50 %-overlap windows in place from the streams' mono buffers, then K5).
+    tensor or a host array). Per push the whole bank costs ONE K6 launch (aid_resample_batch_split: downmix + polyphase
+    resampling of all S streams, reading the chunk where it lies and each stream's last few frames of the previous
+    chunk from a small history, so chunked output equals whole-signal resampling bit for bit) and ONE extraction +
+    match call over every window the push completed in every stream (aid_query_windows: K1-K3 read the 50 %-overlap
+    windows in place from the streams' mono buffers, then K5).
     The reference's equivalent is one ffmpeg process and one `olaf_c query` per recorded clip
     (audio-ident-ui AudioRecorder.svelte:86-106 -> app/audio/decode.py:41-60 -> app/audio/fingerprint.py:158-219).
     """
@@ -197,13 +198,16 @@ class StreamBank:
         self.win = int(round(window_s * self.sr)) & ~1
         self.hop = int(round(hop_s * self.sr)) & ~1
         self.up, self.down, self.hl, self.J = engine.resample_plan(self.stream_sr, self.sr)
-        self.cap_in = max(int(capacity_s * self.stream_sr), 4 * int(window_s * self.stream_sr)) & ~1
         self.cap_m = max(int(capacity_s * self.sr), 4 * self.win) & ~1
-        self.raw = torch.zeros(self.S, 2 * self.cap_in, dtype=torch.float32, device="cuda")  # [stream][frame][L, R]
+        # K6 history: the input frames the next output still reads that came before the next chunk -- at most J - 1
+        # per stream (the next output's last input has not arrived). Two buffers: the next history is written while
+        # the launch that reads the current one may still be queued.
+        self.hcap = (self.J + 1) & ~1
+        self._hist = [torch.zeros(self.S, 2 * self.hcap, dtype=torch.float32, device="cuda") for _ in range(2)]
+        self.hist_n = 0      # frames held per stream, ending at stream frame n_in
         self.mono = torch.zeros(self.S, self.cap_m, dtype=torch.float32, device="cuda")
         self._pin = None
-        self.raw_base = 0    # stream frame (stream rate) of raw[:, 0]
-        self.raw_filled = 0  # frames held per stream
+        self._cur = None     # device copy of a host chunk
         self.n_in = 0        # frames received per stream
         self.m_next = 0      # next mono sample (index rate) to produce
         self.base = 0        # stream sample (index rate) of mono[:, 0]
@@ -211,34 +215,45 @@ class StreamBank:
         self.next_start = 0  # stream sample of the next window
         self.timings = None  # a list: push() appends (append, resample, windows) host seconds per push (bench)
 
-    def _append_raw(self, chunk, n: int) -> None:
+    def _chunk_dev(self, chunk, n: int):
+        """The chunk on the device as [S, n, 2] with (frame, channel) contiguous per stream: (tensor, stream stride in
+        floats). A device chunk is used in place (a strided slice of a longer stream tensor included)."""
         import torch
 
-        if self.raw_filled + n > self.cap_in:  # compact: keep the input the next output still reads
-            need = max(self.raw_base, (self.m_next * self.down + self.hl) // self.up - (self.J - 1))
-            drop = need - self.raw_base
-            keep = self.raw_filled - drop
-            if keep + n > self.cap_in:
-                raise ValueError("chunk larger than the stream buffer")
-            src = self.raw[:, 2 * drop: 2 * self.raw_filled]
-            self.raw[:, : 2 * keep] = src if keep <= drop else src.clone()  # no overlap: no temporary copy
-            self.raw_base += drop
-            self.raw_filled = keep
-        dst = self.raw[:, 2 * self.raw_filled: 2 * (self.raw_filled + n)]
         if isinstance(chunk, torch.Tensor):
-            # one strided copy: a [S, n, 2] slice of a longer stream tensor is not contiguous, and reshape() had made
-            # a contiguous temporary first (a second 245 MB pass per 256-stream push, ~42 us of GPU time)
-            dst.view(self.S, n, 2).copy_(chunk, non_blocking=True)
-        else:  # host chunk: through a page-locked staging buffer (an async DMA); synced before its next refill
-            x = np.ascontiguousarray(chunk, dtype=np.float32).reshape(self.S, 2 * n)
-            if self._pin is None or self._pin.numel() < x.size:
-                self._pin = torch.empty(x.size, dtype=torch.float32).pin_memory()
-            torch.cuda.current_stream().synchronize()  # the previous chunk has left the staging buffer
-            pin = self._pin[: x.size].view(self.S, 2 * n)
-            pin.numpy()[:] = x
-            dst.copy_(pin, non_blocking=True)
-        self.raw_filled += n
-        self.n_in += n
+            t = chunk if chunk.dtype == torch.float32 else chunk.float()
+            if not t.is_cuda:
+                t = t.cuda()
+            if n > 1 and (t.stride(2) != 1 or t.stride(1) != 2 or t.stride(0) % 2 or t.data_ptr() % 8):
+                t = t.contiguous()
+            return t, (t.stride(0) if self.S > 1 else 2 * n)
+        x = np.ascontiguousarray(chunk, dtype=np.float32).reshape(self.S, 2 * n)
+        if self._pin is None or self._pin.numel() < x.size:
+            self._pin = torch.empty(x.size, dtype=torch.float32).pin_memory()
+        if self._cur is None or self._cur.numel() < x.size:
+            self._cur = torch.empty(x.size, dtype=torch.float32, device="cuda")
+        torch.cuda.current_stream().synchronize()  # the previous chunk has left the staging buffer
+        pin = self._pin[: x.size].view(self.S, 2 * n)
+        pin.numpy()[:] = x
+        cur = self._cur[: x.size].view(self.S, 2 * n)
+        cur.copy_(pin, non_blocking=True)
+        return cur.view(self.S, n, 2), 2 * n
+
+    def _keep_history(self, cur, n: int) -> None:
+        """The next history: stream frames [need, n_in) from the current history and the chunk (a few frames)."""
+        need = max(0, (self.m_next * self.down + self.hl) // self.up - (self.J - 1))
+        keep = self.n_in - need
+        if keep > self.hcap:  # cannot happen: the next output's last input is >= n_in
+            raise AssertionError("K6 history larger than J - 1 frames")
+        old, new = self._hist
+        from_cur = min(keep, n)
+        from_old = keep - from_cur
+        if from_old:
+            new[:, : 2 * from_old] = old[:, 2 * (self.hist_n - from_old): 2 * self.hist_n]
+        if from_cur:
+            new[:, 2 * from_old: 2 * keep] = cur[:, n - from_cur: n].reshape(self.S, 2 * from_cur)
+        self._hist = [new, old]
+        self.hist_n = keep
 
     def push(self, chunk) -> list[list[WindowResult]]:
         """chunk: [S, n, 2] float32 at stream_sr (device tensor or host array). Returns, per stream, the windows this
@@ -260,8 +275,9 @@ class StreamBank:
             raise ValueError("chunk must be [n_streams, n, 2]")
         s = torch.cuda.current_stream().cuda_stream
         t0 = time.perf_counter()
-        if n:
-            self._append_raw(chunk, n)
+        cur, cur_stride = self._chunk_dev(chunk, n) if n else (None, 0)
+        in_base = self.n_in
+        self.n_in += n
         t1 = time.perf_counter()
         last = self.n_in * self.up - 1 - self.hl  # outputs m whose last input floor((m*down + hl)/up) has arrived
         m_ready = last // self.down + 1 if last >= 0 else 0
@@ -276,11 +292,14 @@ class StreamBank:
                 self.mono[:, :keep] = src if keep <= drop else src.clone()
                 self.base += drop
                 self.filled = keep
-            self.eng.resample_batch(self.raw.data_ptr(), 2 * self.cap_in, self.S, self.raw_base, self.raw_filled, 2,
-                                    self.stream_sr, self.sr, self.m_next, count,
-                                    self.mono.data_ptr() + 4 * self.filled, self.cap_m, s)
+            self.eng.resample_batch_split(self._hist[0].data_ptr(), 2 * self.hcap, self.hist_n,
+                                          cur.data_ptr() if n else self._hist[0].data_ptr(), cur_stride, self.S,
+                                          in_base, n, 2, self.stream_sr, self.sr, self.m_next, count,
+                                          self.mono.data_ptr() + 4 * self.filled, self.cap_m, s)
             self.filled += count
             self.m_next = m_ready
+        if n:
+            self._keep_history(cur, n)
         t2 = time.perf_counter()
         starts = []
         while self.next_start + self.win <= self.base + self.filled:

@@ -37,7 +37,8 @@ void launch_synth(float *out, const uint32_t *tracks, const int64_t *starts, int
 int64_t resample_lds_floats(int up, int down, int J);
 void launch_resample(const float *src, int64_t in_base, int64_t n, int channels, int up, int down, int hl, int J,
                      const float *taps, float *dst, int64_t m_first, int64_t count, hipStream_t s, int n_streams = 1,
-                     int64_t src_stride = 0, int64_t dst_stride = 0);
+                     int64_t src_stride = 0, int64_t dst_stride = 0, const float *hist = nullptr, int64_t hist_n = 0,
+                     int64_t hist_stride = 0);
 int dedup_chunks(int64_t n_cat);
 void launch_dedup_scan(const uint32_t *cw, const int64_t *coff, const double *cdur, int64_t n_cat, const uint32_t *qw,
                        const int64_t *qoff, const double *qlo, const double *qhi, int nq, double *part_sim,
@@ -1067,14 +1068,18 @@ int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t
     return aid_resample_batch(e, src, 0, 1, in_base, n, channels, sr_in, sr_out, m_first, count, dst, 0, stream);
 }
 
-int aid_resample_batch(aid_engine *e, const float *src, int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n,
-                       int32_t channels, int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
-                       int64_t dst_stride, void *stream) {
+static int resample_batch(aid_engine *e, const float *src, int64_t src_stride, int32_t n_streams, int64_t in_base,
+                          int64_t n, int32_t channels, int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count,
+                          float *dst, int64_t dst_stride, void *stream, const float *hist, int64_t hist_n,
+                          int64_t hist_stride) {
     if (!e || n < 0 || in_base < 0 || m_first < 0 || count < 0 || (channels != 1 && channels != 2) || n_streams < 0 ||
-        n_streams > 65535 || src_stride < 0 || dst_stride < 0)
+        n_streams > 65535 || src_stride < 0 || dst_stride < 0 || hist_n < 0 || hist_n > in_base || hist_stride < 0)
         return fail(AID_ERR_INVALID, "aid_resample: bad argument");
     if (n_streams > 1 && (src_stride < n * channels || dst_stride < count || (channels == 2 && (src_stride & 1))))
         return fail(AID_ERR_INVALID, "aid_resample_batch: strides must cover one stream (stereo: even)");
+    if (hist_n > 0 && (!hist || (n_streams > 1 && hist_stride < hist_n * channels) ||
+                       (channels == 2 && ((hist_stride & 1) || (reinterpret_cast<uintptr_t>(hist) & 7)))))
+        return fail(AID_ERR_INVALID, "aid_resample_batch_split: bad history (null, stride, or stereo alignment)");
     if (n_streams == 0) return AID_OK;
     ResamplePlan p;
     if (!resample_plan(sr_in, sr_out, p)) return fail(AID_ERR_INVALID, "aid_resample: sample rates must be > 0");
@@ -1093,10 +1098,25 @@ int aid_resample_batch(aid_engine *e, const float *src, int64_t src_stride, int3
     {
         ProfScope ps(e, AID_K_RESAMPLE, s);
         launch_resample(src, in_base, n, channels, p.up, p.down, p.hl, p.J, taps, dst, m_first, count, s, n_streams,
-                        src_stride, dst_stride);
+                        src_stride, dst_stride, hist, hist_n, hist_stride);
     }
     HIP_TRY(hipGetLastError());
     return AID_OK;
+}
+
+int aid_resample_batch(aid_engine *e, const float *src, int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n,
+                       int32_t channels, int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
+                       int64_t dst_stride, void *stream) {
+    return resample_batch(e, src, src_stride, n_streams, in_base, n, channels, sr_in, sr_out, m_first, count, dst,
+                          dst_stride, stream, nullptr, 0, 0);
+}
+
+int aid_resample_batch_split(aid_engine *e, const float *hist, int64_t hist_stride, int64_t hist_n, const float *src,
+                             int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n, int32_t channels,
+                             int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
+                             int64_t dst_stride, void *stream) {
+    return resample_batch(e, src, src_stride, n_streams, in_base, n, channels, sr_in, sr_out, m_first, count, dst,
+                          dst_stride, stream, hist, hist_n, hist_stride);
 }
 
 int aid_resample(aid_engine *e, const float *src, int64_t n, int32_t channels, int32_t sr_in, int32_t sr_out,

@@ -248,6 +248,15 @@ int aid_resample_range(aid_engine *e, const float *src, int64_t in_base, int64_t
 int aid_resample_batch(aid_engine *e, const float *src, int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n,
                        int32_t channels, int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
                        int64_t dst_stride, void *stream);
+/* aid_resample_batch over a two-part input: stream frames [in_base - hist_n, in_base) from hist (hist_stride floats
+ * per stream), then [in_base, in_base + n) from src. A live stream's chunk is read where the caller holds it and only
+ * the previous chunk's last few frames are kept, instead of appending every chunk to a long history first (a
+ * 256-stream 2.5 s push is 246 MB of stereo: its append cost ~80 us of GPU per push). Outputs bit for bit those of
+ * aid_resample_batch over the concatenated input. */
+int aid_resample_batch_split(aid_engine *e, const float *hist, int64_t hist_stride, int64_t hist_n, const float *src,
+                             int64_t src_stride, int32_t n_streams, int64_t in_base, int64_t n, int32_t channels,
+                             int32_t sr_in, int32_t sr_out, int64_t m_first, int64_t count, float *dst,
+                             int64_t dst_stride, void *stream);
 /* (up, down, hl, J) of a rate pair (FPSPEC 8); returns 0 on bad rates */
 int aid_resample_plan(int32_t sr_in, int32_t sr_out, int32_t *up, int32_t *down, int32_t *hl, int32_t *J);
 

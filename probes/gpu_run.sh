@@ -11,6 +11,8 @@
 #   counters  rocprofv3 -L
 #   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/k2pf2 (probes/run_ab_lib.sh, 3 rounds)
 #   ctests the GPU tests of the service, its coalescer and the stream bank only
+#   k6ab   the pipelined stream probe on the product library and two K6 variants (build/k6r4, build/k6old), 3 rounds
+#   svc    the service leg alone (defaults)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
 #   streamprof  probes/stream_host_profile.py (256 streams: push wall time, GPU kernels per push, cProfile)
 #   streamtrace the same probe under rocprofv3 --runtime-trace --kernel-trace (HIP API durations: host waits)
@@ -27,7 +29,7 @@ for step in "$@"; do
   i=$((i + 1))
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 ;;
-    ctests) timeout -k 10 400 python -u -m pytest tests/test_gpu_concurrency.py tests/test_gpu_adapter.py tests/test_gpu_stream.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_ctests.txt 2>&1 ;;
+    ctests) timeout -k 10 400 python -u -m pytest tests/test_gpu_concurrency.py tests/test_gpu_adapter.py tests/test_gpu_stream.py tests/test_gpu_resample.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_ctests.txt 2>&1 ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     bench) timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err ;;
     music) timeout -k 10 900 python3 -u probes/music_eval.py --tracks 1000 --queries 500 --negatives 100 --workers 16 > $O/music.json 2> $O/music.err ;;
@@ -45,6 +47,8 @@ for step in "$@"; do
     counters) timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 ;;
     k2ab) timeout -k 10 900 bash probes/run_ab_lib.sh $O/k2pf2_ab.txt k2pf2 3 > $O/k2ab.log 2>&1 ;;
     streamprof) timeout -k 10 300 python3 probes/stream_host_profile.py > $O/stream_prof.txt 2> $O/stream_prof.err ;;
+    streamprofp) timeout -k 10 300 python3 probes/stream_host_profile.py --pipelined > $O/stream_prof_p.txt 2> $O/stream_prof_p.err ;;
+    streamtracep) timeout -k 10 300 rocprofv3 --runtime-trace --kernel-trace --stats -T -d $O/straceP -o run --output-format csv -- python3 probes/stream_host_profile.py --seconds 30 --pipelined > $O/stream_trace_p.txt 2> $O/stream_trace_p.err ;;
     streamtrace) timeout -k 10 300 rocprofv3 --runtime-trace --kernel-trace --stats -T -d $O/strace -o run --output-format csv -- python3 probes/stream_host_profile.py --seconds 30 > $O/stream_trace.txt 2> $O/stream_trace.err ;;
     k5mm)
       timeout -k 10 400 python3 bench_match.py --no-cpu --category-queries 200 --min-match 10 > $O/k5mm10.json 2> $O/k5mm10.err &&
@@ -53,6 +57,17 @@ for step in "$@"; do
       rc=0
       for r in 1 2; do for v in "0 0" "1 0" "1 16" "1 32"; do set -- $v
         timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-pipeline $1 --service-split-min $2 > $O/svc_p$1_s$2_r$r.json 2> $O/svc_p$1_s$2_r$r.err || { rc=$?; break 2; }
+      done; done
+      [ $rc -eq 0 ] ;;
+    svc)
+      timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/svc.json 2> $O/svc.err ;;
+    k6ab)
+      rc=0
+      for r in 1 2 3; do for lib in product k6r4 k6old; do
+        if [ $lib = product ]; then L=""; else L="AIDFP_LIB=$GRAFT_REPO_ROOT/audio-ident_amd/build/$lib/libaidfp.so"; fi
+        echo "== $lib $r" >> $O/k6ab.txt
+        env $L timeout -k 10 200 python3 probes/stream_host_profile.py --seconds 30 --pipelined > $O/k6_${lib}_$r.txt 2>/dev/null || { rc=$?; break 2; }
+        head -1 $O/k6_${lib}_$r.txt >> $O/k6ab.txt
       done; done
       [ $rc -eq 0 ] ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -113,6 +113,61 @@ def test_resample_batch_equals_single_streams(gpu_engine):
             assert not out_b[i, cnt:].any()
 
 
+def test_resample_batch_split_equals_whole(gpu_engine):
+    """aid_resample_batch_split: a two-part input (the last h frames before stream frame k from a history buffer,
+    frames k.. from the chunk where it lies) gives aid_resample_batch's outputs over the whole input, bit for bit."""
+    rng = np.random.default_rng(9)
+    for sr_in, sr_out, ch in ((48000, 16000, 2), (48000, 44100, 2), (44100, 16000, 1)):
+        up, down, hl, J = gpu_engine.resample_plan(sr_in, sr_out)
+        S, N, k, h = 3, 40000, 20001, J + 3
+        x = rng.standard_normal((S, N * ch + 4)).astype(np.float32)
+        whole = torch.from_numpy(x).cuda()
+        hist = torch.from_numpy(np.ascontiguousarray(x[:, (k - h) * ch: k * ch])).cuda()
+        cur = whole[:, k * ch:]  # in place: a strided view of the whole input
+        m0 = -(-((k - h + J - 1) * up - hl) // down)  # first output whose window starts at or after frame k - h
+        cnt = (N * up - 1 - hl) // down + 1 - m0       # through the last output with its inputs in range
+        a = torch.zeros(S, cnt, dtype=torch.float32, device="cuda")
+        b = torch.zeros(S, cnt, dtype=torch.float32, device="cuda")
+        gpu_engine.resample_batch(whole.data_ptr(), x.shape[1], S, 0, N, ch, sr_in, sr_out, m0, cnt, a.data_ptr(), cnt)
+        gpu_engine.resample_batch_split(hist.data_ptr(), h * ch, h, cur.data_ptr(), x.shape[1], S, k, N - k, ch, sr_in,
+                                        sr_out, m0, cnt, b.data_ptr(), cnt)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), (sr_in, sr_out, ch)
+
+
+@pytest.mark.parametrize("steps", [(37, 1, 5000, 48000), (120000,)])
+def test_stream_bank_chunk_sizes(steps):
+    """StreamBank keeps only the last J - 1 input frames between pushes (the chunk is read in place): pushes of 1,
+    37 and 5000 frames (shorter than the filter: the history comes partly from earlier chunks) and whole 2.5 s
+    pushes give exactly the windows of a per-stream StreamIdentifier."""
+    from aidfp.catalog import ingest_synthetic
+    from aidfp.stream import StreamBank
+
+    with Engine(16000) as eng:
+        ingest_synthetic(eng, np.arange(12, dtype=np.uint32), 30.0, source_sr=44100)
+        orders = [[3, 7], [11, 2]]
+        st = _stereo_streams(orders, 6.0, SR, salt0=40)  # 12 s per stream
+        dev = torch.from_numpy(st).cuda()
+        bank = StreamBank(eng, len(orders), stream_sr=SR)
+        singles = [StreamIdentifier(eng, stream_sr=SR) for _ in orders]
+        got = [[] for _ in orders]
+        want = [[] for _ in orders]
+        a = i = 0
+        while a < st.shape[1]:
+            step = steps[i % len(steps)]
+            i += 1
+            res = bank.push(dev[:, a:a + step])
+            for j in range(len(orders)):
+                got[j] += res[j]
+                want[j] += singles[j].push(st[j, a:a + step])
+            a += step
+        assert bank.hist_n <= bank.J - 1
+        for j in range(len(orders)):
+            assert len(got[j]) == len(want[j]) == int((st.shape[1] / SR - 5.0) // 2.5) + 1
+            for g, w in zip(got[j], want[j]):
+                assert g.start_s == w.start_s and np.array_equal(g.rows, w.rows), (j, g.start_s)
+
+
 def test_stream_bank_equals_oracle_route():
     """The production streaming path: StreamBank with 6 live 48 kHz stereo streams in lockstep
     against a 16 kHz index ingested from 44.1 kHz sources (the reference's deployment shape), pushed in 1.37 s
