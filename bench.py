@@ -908,8 +908,9 @@ def stream_leg(args, rank, world, dist, torch) -> dict:
                                 "max": round(float(lat_ms.max()), 3), "all": [round(float(x), 3) for x in lat_ms]},
             "realtime_factor_per_gpu": round(stream_s / wall_max, 1),
             "top1_inside_segments": round(hits / max(1, inside), 4), "windows_inside_segments": inside,
-            "path": "aidfp.stream.StreamBank: per push one aid_resample_batch (48 kHz stereo -> 16 kHz mono, all "
-                    "streams) + one aid_query_windows (K1-K3 in place over every completed 5 s / 2.5 s-hop window, K5)",
+            "path": "aidfp.stream.StreamBank: per push one aid_resample_batch_split (48 kHz stereo -> 16 kHz mono, all "
+                    "streams, the chunk read in place + each stream's last J - 1 input frames) + one aid_query_windows "
+                    "(K1-K3 in place over every completed 5 s / 2.5 s-hop window, K5)",
             "data": "synthetic 30 s catalog segments at 48 kHz, SNR 30 dB per channel, generated in HBM"})
         if rank == 0 and args.stream_parity_streams > 0:
             try:
@@ -1022,8 +1023,14 @@ def service_leg(args, rank, world, dist, torch) -> dict:
         try:
             def run_levels():
                 res = {}
-                for _ in range(8):  # warm: first-use allocations of the largest batch shape
-                    svc.query(reqs[0])
+                # warm: first-use allocations of the largest batch shape (page-locked staging, the engine's buffers
+                # and a second ticket), i.e. the top level's fan-out, untimed; lone queries warmed only batches of one
+                # and left those allocations inside the top level's first round
+                async def warm():
+                    await asyncio.gather(*(fp.olaf_query(reqs[i % n_req]) for i in range(max(levels))))
+
+                for _ in range(3):
+                    asyncio.run(warm())
                 gc.collect()  # start-up objects out of the cyclic collector's reach, as a serving process does
                 gc.freeze()
                 for c in levels:
