@@ -9,10 +9,12 @@
 #   k5req  the lane's memory-side read requests by size (TCC_EA0_RDREQ, TCC_EA0_RDREQ_32B) and TCP->TCC reads
 #   segv   VERDICT r5 #2: the r05y2 command (service leg under --kernel-trace --memory-copy-trace), once
 #   counters  rocprofv3 -L
-#   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/k2pf2 (probes/run_ab_lib.sh, 3 rounds)
+#   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/$K2AB_VARIANT (probes/run_ab_lib.sh, 3 rounds)
 #   ctests the GPU tests of the service, its coalescer and the stream bank only
 #   k6ab   the pipelined stream probe on the product library and two K6 variants (build/k6r4, build/k6old), 3 rounds
+#   k2mall K1/K2 per step with the clip groups' power plane forced to fit the Infinity Cache (probes/k2_mall_probe.py)
 #   svc    the service leg alone (defaults)
+#   xtests the extraction GPU tests only (K1-K3 parity)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
 #   streamprof  probes/stream_host_profile.py (256 streams: push wall time, GPU kernels per push, cProfile)
 #   streamtrace the same probe under rocprofv3 --runtime-trace --kernel-trace (HIP API durations: host waits)
@@ -30,6 +32,7 @@ for step in "$@"; do
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 ;;
     ctests) timeout -k 10 400 python -u -m pytest tests/test_gpu_concurrency.py tests/test_gpu_adapter.py tests/test_gpu_stream.py tests/test_gpu_resample.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_ctests.txt 2>&1 ;;
+    xtests) timeout -k 10 400 python -u -m pytest tests/test_gpu_extract.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_xtests.txt 2>&1 ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     bench) timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err ;;
     music) timeout -k 10 900 python3 -u probes/music_eval.py --tracks 1000 --queries 500 --negatives 100 --workers 16 > $O/music.json 2> $O/music.err ;;
@@ -45,7 +48,7 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCP_TCC_READ_REQ_sum -T -d $O/k5/req -o run --output-format csv -- $B > $O/k5_req.json 2> $O/k5_req.err ;;
     segv) timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/segv.json 2> $O/segv.err ;;
     counters) timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 ;;
-    k2ab) timeout -k 10 900 bash probes/run_ab_lib.sh $O/k2pf2_ab.txt k2pf2 3 > $O/k2ab.log 2>&1 ;;
+    k2ab) timeout -k 10 900 bash probes/run_ab_lib.sh $O/k2_ab.txt ${K2AB_VARIANT:?set K2AB_VARIANT} 3 > $O/k2ab.log 2>&1 ;;
     streamprof) timeout -k 10 300 python3 probes/stream_host_profile.py > $O/stream_prof.txt 2> $O/stream_prof.err ;;
     streamprofp) timeout -k 10 300 python3 probes/stream_host_profile.py --pipelined > $O/stream_prof_p.txt 2> $O/stream_prof_p.err ;;
     streamtracep) timeout -k 10 300 rocprofv3 --runtime-trace --kernel-trace --stats -T -d $O/straceP -o run --output-format csv -- python3 probes/stream_host_profile.py --seconds 30 --pipelined > $O/stream_trace_p.txt 2> $O/stream_trace_p.err ;;
@@ -59,6 +62,7 @@ for step in "$@"; do
         timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-pipeline $1 --service-split-min $2 > $O/svc_p$1_s$2_r$r.json 2> $O/svc_p$1_s$2_r$r.err || { rc=$?; break 2; }
       done; done
       [ $rc -eq 0 ] ;;
+    k2mall) timeout -k 10 400 python3 probes/k2_mall_probe.py 3 > $O/k2_mall.json 2> $O/k2_mall.err ;;
     svc)
       timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/svc.json 2> $O/svc.err ;;
     k6ab)
