@@ -13,6 +13,7 @@
 #   ctests the GPU tests of the service, its coalescer and the stream bank only
 #   k6ab   the pipelined stream probe on the product library and two K6 variants (build/k6r4, build/k6old), 3 rounds
 #   k2mall K1/K2 per step with the clip groups' power plane forced to fit the Infinity Cache (probes/k2_mall_probe.py)
+#   gloo4  world-4 rehearsal of bench.py's N-rank path on the one GPU (gloo; RCCL refuses two ranks per GPU)
 #   svc    the service leg alone (defaults)
 #   xtests the extraction GPU tests only (K1-K3 parity)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
@@ -63,6 +64,7 @@ for step in "$@"; do
       done; done
       [ $rc -eq 0 ] ;;
     k2mall) timeout -k 10 400 python3 probes/k2_mall_probe.py 3 > $O/k2_mall.json 2> $O/k2_mall.err ;;
+    gloo4) AIDFP_BENCH_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 4 --steps 5 --warmup 2 --no-cpu > $O/gloo4.json 2> $O/gloo4.err ;;
     svc)
       timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/svc.json 2> $O/svc.err ;;
     k6ab)
