@@ -31,7 +31,10 @@ struct ResIn {
 // Stage input samples lo .. lo + cnt - 1 (stream indices) into sx[0 .. cnt), downmixed at load time. The loads go out
 // kStageBatch at a time before their LDS stores: a plain strided loop waits for each load before the next (its trip
 // count is not known at compile time), so a block staging ~12 samples per thread paid ~12 serial memory latencies
-constexpr int kStageBatch = 8;
+#ifndef AID_K6_STAGE_BATCH
+#define AID_K6_STAGE_BATCH 8
+#endif
+constexpr int kStageBatch = AID_K6_STAGE_BATCH;
 template <bool STEREO>
 __device__ __forceinline__ void stage_window(const ResIn &in, int64_t lo, int cnt, float *sx, int tid, int nthreads) {
     const int64_t y = blockIdx.y;

@@ -11,9 +11,10 @@
 #   counters  rocprofv3 -L
 #   k2ab   interleaved same-box A/B of the product library vs audio-ident_amd/build/$K2AB_VARIANT (probes/run_ab_lib.sh, 3 rounds)
 #   ctests the GPU tests of the service, its coalescer and the stream bank only
-#   k6ab   the pipelined stream probe on the product library and two K6 variants (build/k6r4, build/k6old), 3 rounds
+#   k6ab   the pipelined stream probe on the product library and the K6 variants in $K6AB_VARIANTS (build/<v>), 3 rounds
 #   k2mall K1/K2 per step with the clip groups' power plane forced to fit the Infinity Cache (probes/k2_mall_probe.py)
 #   gloo4  world-4 rehearsal of bench.py's N-rank path on the one GPU (gloo; RCCL refuses two ranks per GPU)
+#   k6pmc  SQ, FETCH_SIZE and WRITE_SIZE passes over the 256-stream push probe (K6 and the windowed extraction)
 #   svc    the service leg alone (defaults)
 #   xtests the extraction GPU tests only (K1-K3 parity)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
@@ -65,11 +66,16 @@ for step in "$@"; do
       [ $rc -eq 0 ] ;;
     k2mall) timeout -k 10 400 python3 probes/k2_mall_probe.py 3 > $O/k2_mall.json 2> $O/k2_mall.err ;;
     gloo4) AIDFP_BENCH_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 4 --steps 5 --warmup 2 --no-cpu > $O/gloo4.json 2> $O/gloo4.err ;;
+    k6pmc)
+      P="python3 probes/stream_host_profile.py --seconds 30"
+      timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY -T -d $O/k6pmc/sq -o run --output-format csv -- $P > $O/k6pmc_sq.txt 2> $O/k6pmc_sq.err &&
+      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $O/k6pmc/fetch -o run --output-format csv -- $P > $O/k6pmc_fetch.txt 2> $O/k6pmc_fetch.err &&
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $O/k6pmc/write -o run --output-format csv -- $P > $O/k6pmc_write.txt 2> $O/k6pmc_write.err ;;
     svc)
       timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/svc.json 2> $O/svc.err ;;
     k6ab)
       rc=0
-      for r in 1 2 3; do for lib in product k6r4 k6old; do
+      for r in 1 2 3; do for lib in product ${K6AB_VARIANTS:?set K6AB_VARIANTS}; do
         if [ $lib = product ]; then L=""; else L="AIDFP_LIB=$GRAFT_REPO_ROOT/audio-ident_amd/build/$lib/libaidfp.so"; fi
         echo "== $lib $r" >> $O/k6ab.txt
         env $L timeout -k 10 200 python3 probes/stream_host_profile.py --seconds 30 --pipelined > $O/k6_${lib}_$r.txt 2>/dev/null || { rc=$?; break 2; }
