@@ -15,6 +15,7 @@
 #   k2mall K1/K2 per step with the clip groups' power plane forced to fit the Infinity Cache (probes/k2_mall_probe.py)
 #   gloo4  world-4 rehearsal of bench.py's N-rank path on the one GPU (gloo; RCCL refuses two ranks per GPU)
 #   k6pmc  SQ, FETCH_SIZE and WRITE_SIZE passes over the 256-stream push probe (K6 and the windowed extraction)
+#   k6res  bench_resample.py (256 x 10 s stereo 48 kHz -> 16 / 44.1 kHz) on the product and $K6AB_VARIANTS, 2 rounds
 #   svc    the service leg alone (defaults)
 #   xtests the extraction GPU tests only (K1-K3 parity)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
@@ -71,6 +72,14 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY -T -d $O/k6pmc/sq -o run --output-format csv -- $P > $O/k6pmc_sq.txt 2> $O/k6pmc_sq.err &&
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $O/k6pmc/fetch -o run --output-format csv -- $P > $O/k6pmc_fetch.txt 2> $O/k6pmc_fetch.err &&
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $O/k6pmc/write -o run --output-format csv -- $P > $O/k6pmc_write.txt 2> $O/k6pmc_write.err ;;
+    k6res)
+      rc=0
+      for r in 1 2; do for lib in product ${K6AB_VARIANTS:?set K6AB_VARIANTS}; do
+        if [ $lib = product ]; then L=""; else L="AIDFP_LIB=$GRAFT_REPO_ROOT/audio-ident_amd/build/$lib/libaidfp.so"; fi
+        echo "== $lib $r" >> $O/k6res.txt
+        env $L timeout -k 10 200 python3 bench_resample.py --no-cpu >> $O/k6res.txt 2>/dev/null || { rc=$?; break 2; }
+      done; done
+      [ $rc -eq 0 ] ;;
     svc)
       timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream > $O/svc.json 2> $O/svc.err ;;
     k6ab)
