@@ -16,6 +16,7 @@
 #   gloo4  world-4 rehearsal of bench.py's N-rank path on the one GPU (gloo; RCCL refuses two ranks per GPU)
 #   k6pmc  SQ, FETCH_SIZE and WRITE_SIZE passes over the 256-stream push probe (K6 and the windowed extraction)
 #   k6res  bench_resample.py (256 x 10 s stereo 48 kHz -> 16 / 44.1 kHz) on the product and $K6AB_VARIANTS, 2 rounds
+#   settleab headline only: (steps, settle seconds) = (20, 0.1), (100, 0.1), (100, 0.5), 3 interleaved rounds
 #   svc    the service leg alone (defaults)
 #   xtests the extraction GPU tests only (K1-K3 parity)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
@@ -78,6 +79,14 @@ for step in "$@"; do
         if [ $lib = product ]; then L=""; else L="AIDFP_LIB=$GRAFT_REPO_ROOT/audio-ident_amd/build/$lib/libaidfp.so"; fi
         echo "== $lib $r" >> $O/k6res.txt
         env $L timeout -k 10 200 python3 bench_resample.py --no-cpu >> $O/k6res.txt 2>/dev/null || { rc=$?; break 2; }
+      done; done
+      [ $rc -eq 0 ] ;;
+    settleab)
+      rc=0
+      for r in 1 2 3; do for v in "20 0.1" "100 0.1" "100 0.5"; do set -- $v
+        echo "== steps $1 settle $2 round $r" >> $O/settle_ab.txt
+        timeout -k 10 200 python3 bench.py --steps $1 --settle $2 --no-cpu --no-fullband --no-catalog --no-service --no-stream > $O/settle_tmp.json 2>/dev/null || { rc=$?; break 2; }
+        tail -1 $O/settle_tmp.json | cut -c1-220 >> $O/settle_ab.txt
       done; done
       [ $rc -eq 0 ] ;;
     svc)
