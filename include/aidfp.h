@@ -338,7 +338,8 @@ int aid_query_windows(aid_engine *e, const float *pcm, const int64_t *starts, co
  * kernels). _submit enqueues the extraction, K5 and the result copies on `stream` and returns a ticket at once;
  * _collect waits for that ticket's work, answers any query the fast match path handed back, writes the rows exactly
  * as aid_query_windows would and hands the ticket back to the engine's pool (also on error). Tickets may be collected
- * in any order; the windows' PCM must stay unchanged until the ticket's work has run (it is read in stream order). */
+ * in any order; the windows' PCM must stay unchanged until the ticket's work has run (it is read in stream order).
+ * Collect every ticket before aid_engine_destroy (the engine frees its pooled tickets, not the outstanding ones). */
 typedef struct aid_query_ticket aid_query_ticket;
 int aid_query_windows_submit(aid_engine *e, const float *pcm, const int64_t *starts, const int64_t *ends,
                              int32_t n_windows, void *stream, aid_query_ticket **ticket);
