@@ -21,6 +21,7 @@ Here the index lives in one GPU engine:
 from __future__ import annotations
 
 import asyncio
+import collections
 import logging
 import queue
 import threading
@@ -138,7 +139,8 @@ class QueryCoalescer:
 
     def __init__(self, run_batch: Callable[[Sequence], Sequence], window_s: float = 0.0005, max_batch: int = 256,
                  max_batch_bytes: int = 64 << 20, workers: int = 1,
-                 submit_batch: Callable[[Sequence, bool], object] | None = None, split_min: int = 0):
+                 submit_batch: Callable[[Sequence, bool], object] | None = None, split_min: int = 0,
+                 split_parts: int = 2):
         self._run = run_batch
         # pipelined dispatch: submit_batch(payloads, behind) starts a batch and returns a handle
         # whose collect() gives the results; the dispatcher starts batch N + 1 before it collects batch N, so one
@@ -151,6 +153,7 @@ class QueryCoalescer:
         # outstanding is started as two halves, so the first half's answers (and its clients' next requests) overlap
         # the second half's copy and kernels.
         self.split_min = int(split_min)
+        self.split_parts = max(2, int(split_parts))  # parts of a split batch = batches in flight at most
         self.window_s = float(window_s)
         self.max_batch = int(max_batch)
         self.max_batch_bytes = int(max_batch_bytes)
@@ -233,47 +236,51 @@ class QueryCoalescer:
 
     def _loop(self) -> None:
         pipelined = self._submit is not None and self.workers == 1
+        depth = self.split_parts  # batches in flight at most (pipelined dispatch)
         held = None  # the request that did not fit this thread's previous batch
-        pending = None  # (live requests, handle, exception) of the batch in flight (pipelined dispatch)
+        inflight: collections.deque = collections.deque()  # (live requests, handle, exception), oldest first
         while True:
             if held is not None:
                 first, held = held, None
-            elif pending is None:
+            elif not inflight:
                 first = self._q.get()
             else:
                 try:
                     first = self._q.get_nowait()
-                except queue.Empty:  # nothing to overlap the batch in flight with: answer it now
-                    self._finish(*pending)
-                    pending = None
+                except queue.Empty:  # nothing to overlap the oldest batch in flight with: answer it now
+                    self._finish(*inflight.popleft())
                     continue
             if first is _STOP:
-                if pending is not None:
-                    self._finish(*pending)
+                while inflight:
+                    self._finish(*inflight.popleft())
                 return
             batch, held, stop = self._gather(first)
             if pipelined:
-                if pending is None and self.split_min and len(batch) >= self.split_min:
-                    h = len(batch) // 2
-                    live = self._live(batch[:h])
-                    pending = self._start(live, False) if live else None
-                    batch = batch[h:]
-                live = self._live(batch)
-                started = self._start(live, pending is not None) if live else None
-                if started is _BUSY:  # the runner cannot start this batch beside the outstanding one
-                    self._finish(*pending)
-                    pending = None
-                    started = self._start(live, False)
-                elif started is not None and pending is not None:
-                    self.overlapped += 1
-                if pending is not None:
-                    self._finish(*pending)
-                pending = started
+                parts = [batch]
+                if not inflight and self.split_min and len(batch) >= self.split_min:
+                    k = min(depth, len(batch))
+                    parts = [batch[i * len(batch) // k:(i + 1) * len(batch) // k] for i in range(k)]
+                for part in parts:
+                    live = self._live(part)
+                    if not live:
+                        continue
+                    while len(inflight) >= depth:
+                        self._finish(*inflight.popleft())
+                    started = self._start(live, bool(inflight))
+                    if started is _BUSY:  # the runner cannot start this batch beside the outstanding ones
+                        while inflight:
+                            self._finish(*inflight.popleft())
+                        started = self._start(live, False)
+                    elif inflight:
+                        self.overlapped += 1
+                    inflight.append(started)
+                while len(inflight) > depth - 1:  # the newest stays in flight while the next batch gathers
+                    self._finish(*inflight.popleft())
             else:
                 self._dispatch(batch)
             if stop:
-                if pending is not None:
-                    self._finish(*pending)
+                while inflight:
+                    self._finish(*inflight.popleft())
                 if held is not None:
                     self._dispatch([held])
                 return

@@ -140,7 +140,7 @@ class FingerprintService:
 
     def __init__(self, db_dir: Path | None = None, device: int = -1, checkpoint_min_bytes: int = 64 << 20,
                  coalesce_window_s: float = 0.0005, max_batch: int = 256, max_batch_bytes: int = 64 << 20,
-                 coalesce_workers: int = 1, pipeline: bool = True, split_min: int = 16):
+                 coalesce_workers: int = 1, pipeline: bool = True, split_min: int = 16, split_parts: int = 2):
         self.db_dir = Path(db_dir) if db_dir is not None else db_path()
         self.device = device
         self._rw = RWLock()  # index writers exclusive, queries shared
@@ -149,7 +149,8 @@ class FingerprintService:
         # 16 kHz audio): many long uploads cannot land in one extraction
         # pipeline: the coalescer starts batch N + 1 (aid_query_pcm_submit) before it collects batch N
         self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch, max_batch_bytes,
-                                         coalesce_workers, self._submit_batch if pipeline else None, split_min)
+                                         coalesce_workers, self._submit_batch if pipeline else None, split_min,
+                                         split_parts)
         self._ckpt_retry_at = 0.0  # monotonic time before which a failed auto-checkpoint is not retried
         self._engine = None
         self._store = None

@@ -988,7 +988,7 @@ def service_leg(args, rank, world, dist, torch) -> dict:
     with tempfile.TemporaryDirectory() as db:
         svc = fp.FingerprintService(Path(db), device=torch.cuda.current_device(),
                                     coalesce_workers=args.service_workers, pipeline=bool(args.service_pipeline),
-                                    split_min=args.service_split_min)
+                                    split_min=args.service_split_min, split_parts=args.service_split_parts)
         svc.persist = False
 
         def build():
@@ -1082,6 +1082,7 @@ def service_leg(args, rank, world, dist, torch) -> dict:
                       "sources": "scripts/eval_exact.py:53 (p95 <= 2000 ms); app/search/orchestrator.py:31 (3 s)"}
     out["pipelined"] = bool(args.service_pipeline)
     out["split_min"] = args.service_split_min if args.service_pipeline else None
+    out["split_parts"] = args.service_split_parts if args.service_pipeline else None
     out["path"] = ("aidfp.fingerprint.olaf_query -> QueryCoalescer -> "
                    + ("aid_query_pcm_submit / _collect, batch N + 1 submitted before batch N is collected"
                       if args.service_pipeline else "aid_query_pcm")
@@ -1128,6 +1129,8 @@ def main() -> int:
     ap.add_argument("--service-split-min", type=int, default=16,
                     help="pipelined: a batch of at least this many requests gathered with none in flight runs as two "
                          "halves (0: never split)")
+    ap.add_argument("--service-split-parts", type=int, default=2,
+                    help="pipelined: parts of a split batch (= batches in flight at most)")
     ap.add_argument("--service-requests", type=int, default=512)
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print one line per rank and exit without touching the GPU (tests)")

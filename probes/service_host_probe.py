@@ -75,9 +75,9 @@ class FakeEngine:
 
 
 def run(workers: int, clients: int, n_req: int, gpu_ms: float, rows: int, pipeline: bool = False,
-        max_batch: int = 256, split_min: int = 0) -> dict:
+        max_batch: int = 256, split_min: int = 0, split_parts: int = 2) -> dict:
     svc = fp.FingerprintService(Path("/tmp/aidfp_probe_db"), coalesce_workers=workers, pipeline=pipeline,
-                                max_batch=max_batch, split_min=split_min)
+                                max_batch=max_batch, split_min=split_min, split_parts=split_parts)
     svc.persist = False
     svc._engine = FakeEngine(gpu_ms, rows)
     svc._names = {i: f"track-{i}" for i in range(1000)}
@@ -109,7 +109,8 @@ def run(workers: int, clients: int, n_req: int, gpu_ms: float, rows: int, pipeli
     b = np.array(svc._coalescer.batches)
     fp.set_service(None)
     svc.close()
-    return {"workers": workers, "pipeline": pipeline, "max_batch": max_batch, "split_min": split_min, "overlapped": svc._coalescer.overlapped,
+    return {"workers": workers, "pipeline": pipeline, "max_batch": max_batch, "split_min": split_min,
+            "split_parts": split_parts, "overlapped": svc._coalescer.overlapped,
             "clients": clients, "gpu_ms": gpu_ms, "qps": round(n_req / wall, 1),
             "p50_ms": round(1e3 * float(np.percentile(lat, 50)), 3), "p95_ms": round(1e3 * float(np.percentile(lat, 95)), 3),
             "mean_batch": round(float(b.mean()), 2)}
@@ -125,21 +126,22 @@ def main():
     ap.add_argument("--pipeline", type=int, nargs="+", default=[0], help="0/1: the coalescer's pipelined dispatch")
     ap.add_argument("--max-batch", type=int, nargs="+", default=[256])
     ap.add_argument("--split-min", type=int, nargs="+", default=[0])
+    ap.add_argument("--split-parts", type=int, nargs="+", default=[2])
     ap.add_argument("--profile", action="store_true")
     a = ap.parse_args()
-    for w, pl, mb, sm in [(w, pl, mb, sm) for w in a.workers for pl in a.pipeline for mb in a.max_batch
-                          for sm in a.split_min]:
+    for w, pl, mb, sm, sp in [(w, pl, mb, sm, sp) for w in a.workers for pl in a.pipeline for mb in a.max_batch
+                              for sm in a.split_min for sp in a.split_parts]:
         if a.profile:
             import cProfile
             import pstats
 
             pr = cProfile.Profile()
             pr.enable()
-            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows, bool(pl), mb, sm)
+            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows, bool(pl), mb, sm, sp)
             pr.disable()
             pstats.Stats(pr).sort_stats("tottime").print_stats(18)
         else:
-            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows, bool(pl), mb, sm)
+            r = run(w, a.clients, a.requests, a.gpu_ms, a.rows, bool(pl), mb, sm, sp)
         print(json.dumps(r), flush=True)
 
 
