@@ -74,7 +74,11 @@ __device__ __forceinline__ uint64_t group16(uint64_t m) {
 
 // power-row store, non-temporal (streaming): K1 0.268 -> 0.266 ms, K2 0.134 -> 0.130 ms same-box (r02)
 __device__ __forceinline__ void pstore(float *p, float v) {
+#if defined(AID_K1_NOSTORE)  // timing-only diagnostic build: what K1's power stores cost (results are wrong)
+    asm volatile("" ::"v"(v), "v"(p));
+#else
     __builtin_nontemporal_store(v, p);
+#endif
 }
 
 // E3 slot of Z[k] = 4 (k & 255) + (j2 ^ 2 h), j2 = k >> 8, h = bit 3 of k: the four Z[k + 256 j2] sit in one
