@@ -17,7 +17,9 @@
 #   k6pmc  SQ, FETCH_SIZE and WRITE_SIZE passes over the 256-stream push probe (K6 and the windowed extraction)
 #   k6res  bench_resample.py (256 x 10 s stereo 48 kHz -> 16 / 44.1 kHz) on the product and $K6AB_VARIANTS, 2 rounds
 #   settleab headline only: (steps, settle seconds) = (20, 0.1), (100, 0.1), (100, 0.5), 3 interleaved rounds
+#   k5ab   bench_match.py (config 4 lane) on the product and $K5AB_VARIANTS, 2 rounds
 #   svc    the service leg alone (defaults)
+#   mtests the match GPU tests only (K4/K5 parity, lane)
 #   xtests the extraction GPU tests only (K1-K3 parity)
 #   svcab  the service leg: synchronous dispatch, pipelined without / with batch splitting (16, 32), 2 rounds
 #   streamprof  probes/stream_host_profile.py (256 streams: push wall time, GPU kernels per push, cProfile)
@@ -36,6 +38,7 @@ for step in "$@"; do
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.txt 2>&1 ;;
     ctests) timeout -k 10 400 python -u -m pytest tests/test_gpu_concurrency.py tests/test_gpu_adapter.py tests/test_gpu_stream.py tests/test_gpu_resample.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_ctests.txt 2>&1 ;;
+    mtests) timeout -k 10 600 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_match_load.py tests/test_gpu_lane_parity.py tests/test_gpu_exact.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_mtests.txt 2>&1 ;;
     xtests) timeout -k 10 400 python -u -m pytest tests/test_gpu_extract.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_xtests.txt 2>&1 ;;
     smoke) timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 ;;
     bench) timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err ;;
@@ -87,6 +90,15 @@ for step in "$@"; do
         echo "== steps $1 settle $2 round $r" >> $O/settle_ab.txt
         timeout -k 10 200 python3 bench.py --steps $1 --settle $2 --no-cpu --no-fullband --no-catalog --no-service --no-stream > $O/settle_tmp.json 2>/dev/null || { rc=$?; break 2; }
         tail -1 $O/settle_tmp.json | cut -c1-220 >> $O/settle_ab.txt
+      done; done
+      [ $rc -eq 0 ] ;;
+    k5ab)
+      rc=0
+      for r in 1 2; do for lib in product ${K5AB_VARIANTS:?set K5AB_VARIANTS}; do
+        if [ $lib = product ]; then L=""; else L="AIDFP_LIB=$GRAFT_REPO_ROOT/audio-ident_amd/build/$lib/libaidfp.so"; fi
+        echo "== $lib $r" >> $O/k5ab.txt
+        env $L timeout -k 10 400 python3 bench_match.py --no-cpu --category-queries 200 > $O/k5ab_tmp.json 2>/dev/null || { rc=$?; break 2; }
+        tail -1 $O/k5ab_tmp.json >> $O/k5ab.txt
       done; done
       [ $rc -eq 0 ] ;;
     svc)
