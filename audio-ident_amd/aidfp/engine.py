@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import os
 import sys
 import threading
 import weakref
@@ -126,9 +127,12 @@ def _register_hook() -> None:
 
 
 _COPY_THREADS = 4
-_COPY_MIN = 1 << 22  # floats (16 MiB): smaller batches are copied by the calling thread alone. Same-box A/B on the
-#                      service leg (profiles/r05w5_service_copy_ab.jsonl): 64 clients (20 MB batches) 26.6-27.5 k qps
-#                      against 24.9-26.4 k single-threaded; from 4 MiB the 16-client batches (5 MB) lost 7-10 %
+# floats (8 MiB): smaller batches are copied by the calling thread alone. Round 5 (profiles/r05w5_service_copy_ab.jsonl,
+# whole 20 MB batches at 64 clients): threaded 26.6-27.5 k qps against 24.9-26.4 k single-threaded, and from 4 MiB the
+# 16-client batches (5 MB) lost 7-10 %. Round 6 splits a 64-request batch into two 10 MB halves, which a 16 MiB bound
+# left single-threaded: 8 MiB gives 33.1-34.0 k qps against 30.1-33.9 k (profiles/r06ai_service_copy_min_ab.jsonl).
+# AIDFP_COPY_MIN_FLOATS overrides it (A/B runs)
+_COPY_MIN = int(os.environ.get("AIDFP_COPY_MIN_FLOATS", 1 << 21))
 _copy_pool = None
 _copy_pool_lock = threading.Lock()
 
