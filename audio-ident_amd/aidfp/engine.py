@@ -126,7 +126,7 @@ def _register_hook() -> None:
         _hook_registered = True
 
 
-_COPY_THREADS = 4
+_COPY_THREADS = int(os.environ.get("AIDFP_COPY_THREADS", 4))  # PCM copy threads; 8 lost 10-16 % at 64 clients (r06aj)
 # floats (8 MiB): smaller batches are copied by the calling thread alone. Round 5 (profiles/r05w5_service_copy_ab.jsonl,
 # whole 20 MB batches at 64 clients): threaded 26.6-27.5 k qps against 24.9-26.4 k single-threaded, and from 4 MiB the
 # 16-client batches (5 MB) lost 7-10 %. Round 6 splits a 64-request batch into two 10 MB halves, which a 16 MiB bound
