@@ -988,7 +988,9 @@ def service_leg(args, rank, world, dist, torch) -> dict:
     with tempfile.TemporaryDirectory() as db:
         svc = fp.FingerprintService(Path(db), device=torch.cuda.current_device(),
                                     coalesce_workers=args.service_workers, pipeline=bool(args.service_pipeline),
-                                    split_min=args.service_split_min, split_parts=args.service_split_parts)
+                                    split_min=args.service_split_min, split_parts=args.service_split_parts,
+                                    coalesce_window_s=None if args.service_window_ms is None
+                                    else args.service_window_ms * 1e-3)
         svc.persist = False
 
         def build():
@@ -1083,6 +1085,7 @@ def service_leg(args, rank, world, dist, torch) -> dict:
     out["pipelined"] = bool(args.service_pipeline)
     out["split_min"] = args.service_split_min if args.service_pipeline else None
     out["split_parts"] = args.service_split_parts if args.service_pipeline else None
+    out["coalesce_window_ms"] = round(svc._coalescer.window_s * 1e3, 3)
     out["path"] = ("aidfp.fingerprint.olaf_query -> QueryCoalescer -> "
                    + ("aid_query_pcm_submit / _collect, batch N + 1 submitted before batch N is collected"
                       if args.service_pipeline else "aid_query_pcm")
@@ -1129,6 +1132,9 @@ def main() -> int:
     ap.add_argument("--service-split-min", type=int, default=16,
                     help="pipelined: a batch of at least this many requests gathered with none in flight runs as two "
                          "halves (0: never split)")
+    ap.add_argument("--service-window-ms", type=float, default=None,
+                    help="the coalescer's collection window after a batch of more than one request (default: the "
+                         "service's, 0 when pipelined)")
     ap.add_argument("--service-split-parts", type=int, default=2,
                     help="pipelined: parts of a split batch (= batches in flight at most)")
     ap.add_argument("--service-requests", type=int, default=512)
