@@ -21,6 +21,7 @@
 #   copyab the service leg with the PCM copy threaded from 16 MiB (product) or 8 MiB batches, 3 rounds
 #   copythr the service leg with 4 or 8 PCM copy threads, 3 rounds
 #   winab  the service leg with a 0.5 / 0.2 / 1.0 ms coalescing window, 3 rounds
+#   splitab the service leg with split_min 16 / 8 / 32 (or $SPLITAB_MIN), 3 rounds
 #   svc    the service leg alone (defaults)
 #   mtests the match GPU tests only (K4/K5 parity, lane)
 #   xtests the extraction GPU tests only (K1-K3 parity)
@@ -120,6 +121,12 @@ for step in "$@"; do
       rc=0
       for r in 1 2 3; do for w in ${WINAB_MS:-0.5 0.2 1.0}; do
         timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-window-ms $w > $O/svc_win${w}_r$r.json 2> $O/svc_win${w}_r$r.err || { rc=$?; break 2; }
+      done; done
+      [ $rc -eq 0 ] ;;
+    splitab)
+      rc=0
+      for r in 1 2 3; do for m in ${SPLITAB_MIN:-16 8 32}; do
+        timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu --no-fullband --no-catalog --no-stream --service-split-min $m > $O/svc_split${m}_r$r.json 2> $O/svc_split${m}_r$r.err || { rc=$?; break 2; }
       done; done
       [ $rc -eq 0 ] ;;
     svc)
