@@ -151,8 +151,8 @@ class FingerprintService:
         # batch then gathers while the current one is in flight, so a pipelined coalescer waits for no window:
         # 40-45 k qps at 64 clients and 27 k at 16 with none, against 30-34 k and 14 k with 0.5 ms
         # (profiles/r06akl_service_window_ab.jsonl); the one-call path keeps its 0.5 ms window
-        if coalesce_window_s is None:
-            coalesce_window_s = 0.0 if pipeline else 0.0005
+        if coalesce_window_s is None:  # (the coalescer pipelines with one dispatcher thread only)
+            coalesce_window_s = 0.0 if pipeline and coalesce_workers == 1 else 0.0005
         self._coalescer = QueryCoalescer(self._query_batch, coalesce_window_s, max_batch, max_batch_bytes,
                                          coalesce_workers, self._submit_batch if pipeline else None, split_min,
                                          split_parts)
