@@ -562,6 +562,9 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
         pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
         w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a full call is sized here
         run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
+        if dist is not None:  # the ranks' timed lanes start together (ranks sharing a GPU in a gloo rehearsal
+            torch.cuda.synchronize()  # otherwise time one rank's lane against another's catalog build)
+            dist.barrier()
         res, t_gpu = run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, True, keep=sel)
         kept = res.pop("kept", {})
         # untimed: the same clips again with events on the K5 kernels and the posting counters
