@@ -558,13 +558,21 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
     sel = np.sort(np.concatenate([prng.choice(n_pos, min(n_pos, n_chk - n_chk_neg), replace=False),
                                   n_pos + prng.choice(n_neg, n_chk_neg, replace=False)]).astype(np.int64))
 
-    def local():
+    def warm():
         pcm = torch.empty(min(n, batch) * clip_n, dtype=torch.float32, device="cuda")
         w = min(n, batch)  # warm-up at the full call size: the engine's scratch for a full call is sized here
         run_batches(a, eng, truth[:w], starts[:w], w, cat, pcm, clip_n, False)
-        if dist is not None:  # the ranks' timed lanes start together (ranks sharing a GPU in a gloo rehearsal
-            torch.cuda.synchronize()  # otherwise time one rank's lane against another's catalog build)
-            dist.barrier()
+        torch.cuda.synchronize()
+        return pcm
+
+    # agreed, then a barrier: the ranks' timed lanes start together (ranks sharing a GPU in a gloo rehearsal would
+    # otherwise time one rank's lane against another rank's catalog build)
+    pcm = _agreed(warm, "exact lane (warm-up)", dist)
+    if dist is not None:
+        dist.barrier()
+
+    def local():
+        nonlocal pcm
         res, t_gpu = run_batches(a, eng, truth, starts, n_pos, cat, pcm, clip_n, True, keep=sel)
         kept = res.pop("kept", {})
         # untimed: the same clips again with events on the K5 kernels and the posting counters
@@ -576,7 +584,7 @@ def exact_leg(eng, args, rank, world, dist, torch) -> dict:
         prof = eng.profile_read(reset=True)
         eng.profile_enable(False)
         ms = eng.match_stats(reset=True)
-        del pcm
+        pcm = None  # the clip buffer goes before the parity check's own allocations
         par = lane_parity(eng, truth, starts, n_pos, sel, kept, cat, torch) if len(sel) else None
         return res, t_gpu, prof, ms, par
 
